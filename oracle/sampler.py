@@ -1,0 +1,108 @@
+"""ORACLE (test infrastructure only) — reverse-diffusion sampler and transitions.
+
+Restates, in fp32 with the reference's operation order:
+  get_x_T              model/diffusion.py:281-300
+  get_x_T_conditional  model/diffusion.py:302-320
+  p_transition         model/diffusion.py:177-190
+  p_transition_sr3     model/diffusion.py:164-175
+  p_transition_supportive   model/diffusion.py:192-209
+  p_transition_conditional  model/diffusion.py:211-223
+  SDDM.infer (continuous=False)  model/model.py:50-124 (loop 106-122)
+  SDDM_spectrogram.infer         model/model.py:212-257
+
+Noise: ``oracle.philox.normal(seed, draw, shape, row_offset)`` with draw 0 for
+x_T and draw t for the transition at step t (t > 1).
+"""
+import numpy as np
+
+from . import philox
+
+f32 = np.float32
+MODES = ("original", "condition_in", "sr3", "supportive", "conditional")
+
+
+def get_x_T(tab, cond, noise):
+    T = len(tab["betas"]) - 1
+    s = tab["sqrt_alpha_bar"][T]
+    return (s * cond + np.sqrt(f32(1.0) - s * s) * noise).astype(np.float32)
+
+
+def get_x_T_conditional(tab, cond, noise):
+    T = len(tab["betas"]) - 1
+    return (tab["sqrt_alpha_bar"][T] * cond + tab["sqrt_delta"][T] * noise).astype(np.float32)
+
+
+def transition(mode, tab, x_t, t, eps, cond=None, noise=None):
+    """One p_transition* step; ``noise`` used only when t > 1."""
+    with np.errstate(invalid="ignore"):
+        if mode in ("original", "condition_in"):
+            x = (x_t - tab["predicted_noise_coeff"][t] * eps) / np.sqrt(tab["alphas"][t])
+            if t > 1:
+                x = x + tab["sigma"][t] * noise
+        elif mode == "sr3":
+            x = (x_t - tab["predicted_noise_coeff"][t] * eps) / np.sqrt(tab["alphas"][t])
+            if t > 1:
+                x = x + np.sqrt(tab["betas"][t]) * noise
+        elif mode == "supportive":
+            g = tab["supportive_gamma"][t]
+            mu = x_t - tab["predicted_noise_coeff"][t] * eps
+            x = ((f32(1.0) - g) * mu + g * cond) / np.sqrt(tab["alphas"][t])
+            if t > 1:
+                x = x + max(f32(0.0), tab["supportive_sigma_hat"][t]) * noise
+        elif mode == "conditional":
+            x = tab["c_xt"][t] * x_t + tab["c_yt"][t] * cond - tab["c_epst"][t] * eps
+            if t > 1:
+                x = x + tab["sqrt_delta_estimated"][t] * noise
+        else:
+            raise NotImplementedError(mode)
+    return np.clip(x.astype(np.float32), f32(-1.0), f32(1.0))
+
+
+def initial_state(mode, tab, cond, seed, row_offset=0):
+    """x_T per SDDM.infer (model/model.py:57-68)."""
+    if mode == "supportive":
+        return cond.astype(np.float32).copy()
+    z = philox.normal(seed, 0, cond.shape, row_offset)
+    if mode == "conditional":
+        return get_x_T_conditional(tab, cond, z)
+    if mode == "condition_in":
+        return get_x_T(tab, cond, z)
+    return z
+
+
+def infer(network, tab, cond, mode="condition_in", noise_condition="sqrt_alpha_bar", seed=7,
+          row_offset=0, record=None):
+    """SDDM.infer (model/model.py:50-124): ``network(cond, x_t, noise_level[B]) -> eps``."""
+    T = len(tab["betas"]) - 1
+    B = cond.shape[0]
+    x = initial_state(mode, tab, cond, seed, row_offset)
+    if record is not None:
+        record.append(x.copy())
+    for t in range(T, 0, -1):
+        if noise_condition == "sqrt_alpha_bar":
+            nl = np.full(B, tab["sqrt_alpha_bar"][t], dtype=np.float32)
+        else:
+            nl = np.full(B, float(t), dtype=np.float32)
+        eps = network(cond, x, nl)
+        z = philox.normal(seed, t, x.shape, row_offset) if t > 1 else None
+        x = transition(mode, tab, x, t, eps, cond, z)
+        if record is not None:
+            record.append(x.copy())
+    return x
+
+
+def infer_spectrogram(network, tab, spec, hop_samples, noise_condition="sqrt_alpha_bar", seed=7,
+                      row_offset=0):
+    """SDDM_spectrogram.infer (model/model.py:212-257): x_T = randn(B,1,hop*F)."""
+    T = len(tab["betas"]) - 1
+    B = spec.shape[0]
+    x = philox.normal(seed, 0, (B, 1, hop_samples * spec.shape[-1]), row_offset)
+    for t in range(T, 0, -1):
+        if noise_condition == "sqrt_alpha_bar":
+            nl = np.full(B, tab["sqrt_alpha_bar"][t], dtype=np.float32)
+        else:
+            nl = np.full(B, float(t), dtype=np.float32)
+        eps = network(spec, x, nl)
+        z = philox.normal(seed, t, x.shape, row_offset) if t > 1 else None
+        x = transition("original", tab, x, t, eps, None, z)
+    return x

@@ -1,0 +1,195 @@
+"""Generate golden vectors by running the REFERENCE Python on CPU (build container only).
+
+Usage (from the repo root, with the reference mounted read-only):
+    PYTHONDONTWRITEBYTECODE=1 python tests/golden/gen_golden.py [--reference /root/reference]
+
+The reference is imported read-only; its modules are built with the
+deterministic weights of ``tests/_weights.py`` and ``torch.randn_like`` /
+``torch.randn`` are replaced by the counter-based stream of ``oracle.philox``
+(draw 0 = x_T, draw t = transition noise at step t), exactly the stream the
+HIP kernels generate.  Only inputs and outputs are written (``*.npz`` data
+fixtures, no reference source); the reference never travels to the GPU box.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+
+SCHEDULES = [("linear", 4, 1e-6, 1e-3), ("linear", 50, 1e-6, 1e-3), ("linear", 100, 1e-6, 1e-3),
+             ("linear", 1000, 1e-6, 1e-3), ("linear", 200, 1e-4, 0.02), ("linear", 1000, 1e-6, 0.01),
+             ("linear", 50, 1e-4, 0.05), ("quad", 100, 1e-4, 0.02), ("cosine", 100, 1e-4, 0.02),
+             ("cosine", 1000, 1e-4, 0.02), ("linear", 3, 1e-4, 0.05)]
+UNET_ARGS = dict(in_channel=2, out_channel=1, inner_channel=32, norm_groups=32,
+                 channel_mults=[1, 2, 3, 4, 5], res_blocks=1, dropout=0, segment_len=128,
+                 segment_stride=64)   # config_unet.json "network.args"
+
+
+def sched_key(s):
+    return f"{s[0]}_{s[1]}_{s[2]:g}_{s[3]:g}"
+
+
+class NoiseInjector:
+    """Replaces torch.randn_like / torch.randn with the Philox stream."""
+
+    def __init__(self, torch, philox, seed):
+        self.torch, self.philox, self.seed = torch, philox, seed
+        self.draws = []
+
+    def __enter__(self):
+        t = self.torch
+        self._rl, self._r = t.randn_like, t.randn
+
+        def randn_like(x, *a, **kw):
+            d = self.draws.pop(0)
+            return t.from_numpy(self.philox.normal(self.seed, d, tuple(x.shape)))
+
+        def randn(*shape, **kw):
+            if len(shape) == 1 and isinstance(shape[0], (tuple, list)):
+                shape = tuple(shape[0])
+            d = self.draws.pop(0)
+            return t.from_numpy(self.philox.normal(self.seed, d, tuple(int(s) for s in shape)))
+
+        t.randn_like, t.randn = randn_like, randn
+        return self
+
+    def __exit__(self, *exc):
+        self.torch.randn_like, self.torch.randn = self._rl, self._r
+        assert not self.draws, f"unused draws {self.draws}"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--out", default=HERE)
+    args = ap.parse_args()
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "speech-denoising-diffusion-model-2_amd"))
+    sys.path.insert(0, args.reference)
+    import torch
+    torch.set_num_threads(8)
+    from oracle import philox
+    from oracle.unet import architecture
+    from sddm_hip.synth import noisy_speech
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    from _weights import make_params
+    from model.diffusion import GaussianDiffusion
+    from model.UNetModified2 import UNetModified2, PositionalEncoding
+    from model.model import SDDM
+    out = {}
+
+    # 1. schedule tables (diffusion.py:50-161)
+    for s in SCHEDULES:
+        d = GaussianDiffusion(*s, device="cpu")
+        for k, v in d.state_dict().items():
+            out[f"sched/{sched_key(s)}/{k}"] = v.numpy().copy()
+    np.savez_compressed(os.path.join(args.out, "schedules.npz"), **out)
+
+    # 2. embedding vector (UNetModified2.py:53-55)
+    emb = {"unet_embedding_vector": PositionalEncoding(32).embedding_vector.numpy().copy()}
+
+    def build_unet(n_samples, sched, mode="condition_in", seed=0):
+        d = GaussianDiffusion(*sched, device="cpu")
+        net = UNetModified2(num_samples=n_samples, **UNET_ARGS)
+        m = SDDM(d, net, p_transition=mode)
+        shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+        P = make_params(shapes, seed)
+        net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+        m.eval()
+        return m, d, net
+
+    # 3. state-dict key layout of the three configs (boundary contract)
+    m, _, _ = build_unet(2112, SCHEDULES[2])
+    keys = {"unet_2112_T100": [[k, list(v.shape)] for k, v in m.state_dict().items()]}
+    with open(os.path.join(args.out, "state_dict_keys.json"), "w") as f:
+        json.dump(keys, f, indent=0)
+
+    # 4. transitions, each mode, at a few t (diffusion.py:164-223)
+    tr = {}
+    rng = np.random.default_rng(42)
+    for s in (SCHEDULES[2], SCHEDULES[4]):
+        d = GaussianDiffusion(*s, device="cpu")
+        T = s[1]
+        for mode in ("original", "sr3", "supportive", "conditional"):
+            for t in (T, T // 2, 2, 1):
+                x_t = rng.uniform(-1, 1, (2, 1, 256)).astype(np.float32)
+                eps = rng.standard_normal((2, 1, 256)).astype(np.float32)
+                cond = rng.uniform(-1, 1, (2, 1, 256)).astype(np.float32)
+                key = f"tr/{sched_key(s)}/{mode}/{t}"
+                inj = NoiseInjector(torch, philox, 7)
+                inj.draws = [t] if t > 1 else []
+                with inj:
+                    X, E, C = map(torch.from_numpy, (x_t, eps, cond))
+                    if mode == "original":
+                        y = d.p_transition(X, t, E)
+                    elif mode == "sr3":
+                        y = d.p_transition_sr3(X, t, E)
+                    elif mode == "supportive":
+                        y = d.p_transition_supportive(X, t, E, C)
+                    else:
+                        y = d.p_transition_conditional(X, t, E, C)
+                tr[key + "/x_t"], tr[key + "/eps"], tr[key + "/cond"] = x_t, eps, cond
+                tr[key + "/out"] = y.numpy().copy()
+        # get_x_T variants (diffusion.py:281-320)
+        cond = rng.uniform(-1, 1, (2, 1, 256)).astype(np.float32)
+        for name in ("get_x_T", "get_x_T_conditional"):
+            inj = NoiseInjector(torch, philox, 7)
+            inj.draws = [0]
+            with inj:
+                y = getattr(d, name)(torch.from_numpy(cond))
+            tr[f"tr/{sched_key(s)}/{name}/cond"] = cond
+            tr[f"tr/{sched_key(s)}/{name}/out"] = y.numpy().copy()
+    np.savez_compressed(os.path.join(args.out, "transitions.npz"), **tr)
+
+    # 5. UNet single forward (UNetModified2.py:237-269)
+    fw = {}
+    for N, B in ((2112, 2), (16448, 1)):
+        m, d, net = build_unet(N, SCHEDULES[2])
+        cond = noisy_speech(B, N, seed=1234)
+        x_t = philox.normal(11, 0, (B, 1, N))
+        nl = np.array([0.93, 0.41][:B], dtype=np.float32).reshape(B, 1, 1)
+        with torch.no_grad():
+            y = net(torch.from_numpy(cond), torch.from_numpy(x_t), torch.from_numpy(nl))
+        fw[f"fw/{N}/cond"], fw[f"fw/{N}/x_t"], fw[f"fw/{N}/noise_level"] = cond, x_t, nl.reshape(-1)
+        fw[f"fw/{N}/eps"] = y.numpy().copy()
+    np.savez_compressed(os.path.join(args.out, "unet_forward.npz"), **fw)
+
+    # 6. full SDDM.infer loops (model.py:50-124) with the Philox stream, every mode
+    inf = {}
+    for mode, sched, N, B in (("condition_in", SCHEDULES[0], 2112, 2), ("original", SCHEDULES[10], 2112, 2),
+                              ("sr3", SCHEDULES[10], 2112, 1), ("supportive", SCHEDULES[10], 2112, 1),
+                              ("conditional", SCHEDULES[10], 2112, 1),
+                              ("condition_in", SCHEDULES[1], 16448, 1)):
+        m, d, net = build_unet(N, sched, mode)
+        T = sched[1]
+        cond = noisy_speech(B, N, seed=1234)
+        steps = []
+        orig = d.p_transition, d.p_transition_sr3, d.p_transition_supportive, d.p_transition_conditional
+
+        def rec(fn):
+            def w(*a, **kw):
+                y = fn(*a, **kw)
+                steps.append(y.numpy().copy())
+                return y
+            return w
+        d.p_transition, d.p_transition_sr3, d.p_transition_supportive, d.p_transition_conditional = map(rec, orig)
+        inj = NoiseInjector(torch, philox, 7)
+        inj.draws = ([] if mode == "supportive" else [0]) + list(range(T, 1, -1))
+        with inj, torch.no_grad():
+            y = m.infer(torch.from_numpy(cond))
+        key = f"inf/{mode}/{sched_key(sched)}/{N}x{B}"
+        inf[key + "/cond"] = cond
+        inf[key + "/out"] = y.numpy().copy()
+        if N <= 2112:
+            inf[key + "/steps"] = np.stack(steps)
+    np.savez_compressed(os.path.join(args.out, "unet_infer.npz"), **inf)
+    np.savez_compressed(os.path.join(args.out, "embedding.npz"), **emb)
+    print("wrote fixtures to", args.out)
+
+
+if __name__ == "__main__":
+    main()
