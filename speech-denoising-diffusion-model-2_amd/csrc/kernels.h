@@ -1,0 +1,104 @@
+// Kernel argument structs and host launchers (implemented in kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sddm {
+
+// ---- noise-level embedding + every ResnetBlock's FeatureWiseAffine (UNetModified2.py:49-89) ----
+struct EmbedArgs {
+  const float* noise_levels;  // [R] explicit noise levels, or null -> use table / time step
+  const float* table;         // sqrt_alpha_bar [R] (noise_condition 'sqrt_alpha_bar'), or null
+  int time_step_mode;         // 1: noise level = (float)r ('time_step', model.py:112)
+  int R;                      // rows
+  int dim;                    // inner_channel (embedding width, 32)
+  const float* emb_vec;       // [dim/2] PositionalEncoding.embedding_vector
+  const float* w1; const float* b1;  // Linear(dim, 4dim)
+  const float* w2; const float* b2;  // Linear(4dim, dim)
+  const float* pw; const float* pb;  // concatenated FeatureWiseAffine Linears [SC][dim], [SC] (+conv1 bias)
+  int SC;                     // sum of projected channels
+  float* out;                 // [R][SC]
+};
+hipError_t launch_embed(const EmbedArgs& a, hipStream_t s);
+
+// ---- GroupNorm statistics finalize (nn.GroupNorm, UNetModified2.py:117) ----
+struct GNSrc { const float* stats; int C; int tiles; int n_tile; };
+struct GNArgs {
+  GNSrc a, b;                 // virtual concat of two producers (b.C == 0 if none)
+  const float* gamma; const float* beta;
+  int G; float eps; int B;
+  float* scale; float* shift; // [B][Ca+Cb]
+};
+hipError_t launch_gn_finalize(const GNArgs& a, hipStream_t s);
+
+// ---- framing + first Conv2d(2 -> C) (UNetModified2.py:23-28, 177-178, 244-247) ----
+struct ConvInArgs {
+  const float* cond; const float* x;  // [B][N] fp32
+  int N, F, W, S;             // samples, frames, segment_len, segment_stride
+  int Cout;                   // 32
+  const float* w;             // [Cout][2][3][3] fp32
+  const float* bias;          // [Cout]
+  void* out;                  // [B][F][W][Cout] (T)
+  float* stats;               // [B][tiles][Cout][2]
+  int TR;                     // frame rows per block
+  int* t_dev;                 // step counter decremented once per launch (may be null)
+};
+hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s);
+
+// ---- MFMA implicit-GEMM 3x3 convolution (Block / Downsample / Upsample / ResnetBlock) ----
+struct ConvArgs {
+  const void* srcA; const void* srcB; int CA, CB;  // virtual channel concat (UNetModified2.py:263)
+  int Hi, Wi;                 // stored source dims
+  int Ho, Wo;                 // output dims
+  int upsample;               // stride-1 kernel reads a nearest-2x upsampled source (UNetModified2.py:96-100)
+  int TR, TW, tiles_x, n_tiles;
+  const float* gn_scale; const float* gn_shift;    // [B][CA+CB] or null (no GN / SiLU prologue)
+  const void* wgt;            // packed [Cout_pad][Cin/32][9][32] (T)
+  const float* bias;          // [Cout]
+  const float* temb; int temb_ld; const int* t_dev; int temb_per_b;  // + temb row (ResnetBlock.noise_func)
+  int Cout;
+  int res_mode;               // 0 none, 1 identity (res_src [B][Ho][Wo][Cout]), 2 conv1x1 over raw concat
+  const void* res_src;        // identity residual
+  const void* rawA; const void* rawB; int RCA, RCB;  // 1x1 residual input (ResnetBlock.res_conv, UNetModified2.py:135)
+  const void* res_wgt;        // packed [Cout_pad][RCA+RCB] (T)
+  void* out;                  // [B][Ho][Wo][Cout]
+  float* stats;               // [B][n_tiles][Cout][2] (sum, M2 about tile mean) or null
+};
+struct ConvCfg { int stride2; int nblk; int mblk; };
+hipError_t launch_conv3x3(int dtype, const ConvCfg& cfg, const ConvArgs& a, int B, hipStream_t s);
+size_t conv3x3_lds_bytes(int dtype, const ConvCfg& cfg, const ConvArgs& a);
+
+// ---- final Block(C -> 1) + overlapAdd + p_transition (UNetModified2.py:235,267-268; diffusion.py:164-223) ----
+struct TransCoef {            // device pointers to the GaussianDiffusion buffers [T+1]
+  const float* betas; const float* alphas; const float* sqrt_alpha_bar; const float* pnc;
+  const float* sigma; const float* sgamma; const float* ssh; const float* sqrt_delta;
+  const float* c_xt; const float* c_yt; const float* c_epst; const float* sde;
+};
+struct FinalArgs {
+  const void* src; int C;     // [B][F][W][C] (T)
+  const float* gn_scale; const float* gn_shift;  // [B][C]
+  const float* w; float bias; // [C][3][3] fp32 (out_channel = 1)
+  int N, F, W, S, FT;
+  int mode;                   // -1: write eps (network forward); else sddm_transition mode
+  float* eps_out;             // mode -1
+  float* x;                   // [B][N] state, updated in place
+  const float* cond;          // [B][N]
+  const int* t_dev;
+  TransCoef co;
+  uint64_t seed; int64_t row_offset;
+};
+hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s);
+
+// ---- standalone transition / initial state (diffusion.py:164-223, 281-320; model.py:57-68) ----
+struct TransArgs {
+  int mode; const float* x_t; const float* eps; const float* cond; float* out;
+  int64_t total; int64_t N; int t; const int* t_dev; TransCoef co; uint64_t seed; int64_t row_offset;
+};
+hipError_t launch_transition(const TransArgs& a, hipStream_t s);
+struct InitArgs {
+  int mode; const float* cond; float* out; int64_t total; int64_t N; int T; TransCoef co; uint64_t seed; int64_t row_offset;
+};
+hipError_t launch_init_state(const InitArgs& a, hipStream_t s);
+hipError_t launch_set_int(int* p, int v, hipStream_t s);
+
+}  // namespace sddm

@@ -1,0 +1,1004 @@
+// libsddm_hip runtime: context, parameter registry, weight packing, per-batch execution plan of
+// one UNetModified2 reverse-diffusion step, and the C ABI declared in include/sddm_hip.h.
+//
+// Reference counterparts:
+//   sddm_configure      ConfigParser.init_obj('diffusion'|'network'|'arch') (parse_config.py:82-95)
+//   sddm_load_param     model.load_state_dict (infer.py:46-51)
+//   sddm_sample         SDDM.infer (model/model.py:50-124)
+//   sddm_network_forward UNetModified2.forward (model/UNetModified2.py:237-269)
+//   sddm_transition     GaussianDiffusion.p_transition* (model/diffusion.py:164-223)
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/sddm_hip.h"
+#include "json_mini.h"
+#include "kernels.h"
+#include "sddm_common.h"
+
+namespace sddm {
+int compute_schedule(const std::string& schedule, int T, double linear_start, double linear_end,
+                     float* out);
+}
+using namespace sddm;
+
+static thread_local std::string g_last_error;
+static void sddm_set_error(int code, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  (void)code;
+}
+#define FAIL(code, ...)                 \
+  do {                                  \
+    sddm_set_error(code, __VA_ARGS__);  \
+    return code;                        \
+  } while (0)
+
+static const char* kTableNames[14] = {"betas", "alphas", "alpha_bar", "sqrt_alpha_bar",
+                                      "predicted_noise_coeff", "sigma", "supportive_gamma",
+                                      "supportive_sigma_hat", "m", "sqrt_delta", "c_xt", "c_yt",
+                                      "c_epst", "sqrt_delta_estimated"};
+
+// ---------------------------------------------------------------------------------------------
+// fp32 -> storage dtype (round to nearest even) on the host
+// ---------------------------------------------------------------------------------------------
+static uint16_t f32_to_bf16_bits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+static uint16_t f32_to_f16_bits(float f) {
+  _Float16 h = (_Float16)f;
+  uint16_t r;
+  std::memcpy(&r, &h, 2);
+  return r;
+}
+static size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
+static void store_elem(void* base, size_t idx, float v, int dt) {
+  if (dt == DT_F32) ((float*)base)[idx] = v;
+  else if (dt == DT_BF16) ((uint16_t*)base)[idx] = f32_to_bf16_bits(v);
+  else ((uint16_t*)base)[idx] = f32_to_f16_bits(v);
+}
+
+// ---------------------------------------------------------------------------------------------
+// device arena (one hipMalloc, bump allocation, 256-B alignment)
+// ---------------------------------------------------------------------------------------------
+struct Arena {
+  char* base = nullptr;
+  size_t cap = 0, used = 0;
+  std::vector<std::pair<size_t, size_t>> pending;  // (offset, bytes) reservations before alloc
+  size_t reserve(size_t bytes) {
+    const size_t off = (used + 255) & ~(size_t)255;
+    used = off + bytes;
+    return off;
+  }
+  hipError_t commit() {
+    if (base) { (void)hipFree(base); base = nullptr; }
+    cap = used;
+    if (cap == 0) return hipSuccess;
+    hipError_t e = hipMalloc(&base, cap);
+    if (e == hipSuccess) e = hipMemset(base, 0, cap);
+    return e;
+  }
+  void reset() {
+    if (base) (void)hipFree(base);
+    base = nullptr; cap = used = 0;
+  }
+  template <typename T> T* at(size_t off) const { return (T*)(base + off); }
+};
+
+// ---------------------------------------------------------------------------------------------
+// UNetModified2 architecture (UNetModified2.py:146-235)
+// ---------------------------------------------------------------------------------------------
+struct UNetCfg {
+  int in_channel = 2, out_channel = 1, inner = 32, groups = 32, res_blocks = 3;
+  std::vector<int> mults{1, 2, 3, 4, 5};
+  int seg = 128, stride = 64;
+  double dropout = 0.0;
+};
+struct LayerDesc { int kind; std::string name; int cin, cout; };  // kind 0 conv,1 res,2 down,3 up,4 final
+static std::vector<LayerDesc> unet_layers(const UNetCfg& c, std::vector<LayerDesc>* downs_out,
+                                          std::vector<LayerDesc>* mid_out, std::vector<LayerDesc>* ups_out) {
+  std::vector<LayerDesc> downs, mid, ups;
+  downs.push_back({0, "downs.0", c.in_channel, c.inner});
+  std::vector<int> feat{c.inner};
+  int cin = c.inner, idx = 1, cout = c.inner;
+  for (size_t ind = 0; ind < c.mults.size(); ++ind) {
+    cout = c.inner * c.mults[ind];
+    for (int r = 0; r < c.res_blocks; ++r) {
+      downs.push_back({1, "downs." + std::to_string(idx++), cin, cout});
+      feat.push_back(cout);
+      cin = cout;
+    }
+    downs.push_back({2, "downs." + std::to_string(idx++), cout, cout});
+    feat.push_back(cout);
+  }
+  mid.push_back({1, "mid.0", cin, cin});
+  idx = 0;
+  for (int ind = (int)c.mults.size() - 1; ind >= 0; --ind) {
+    cin = c.inner * c.mults[ind];
+    cout = cin;
+    ups.push_back({1, "ups." + std::to_string(idx++), cin + feat.back(), cout});
+    feat.pop_back();
+    ups.push_back({3, "ups." + std::to_string(idx++), cout, cout});
+    cout = ind == 0 ? c.inner : c.inner * c.mults[ind - 1];
+    for (int r = 0; r < c.res_blocks; ++r) {
+      ups.push_back({1, "ups." + std::to_string(idx++), cin + feat.back(), cout});
+      feat.pop_back();
+      cin = cout;
+    }
+  }
+  std::vector<LayerDesc> all;
+  all.insert(all.end(), downs.begin(), downs.end());
+  all.insert(all.end(), mid.begin(), mid.end());
+  all.insert(all.end(), ups.begin(), ups.end());
+  all.push_back({4, "final_conv", cout, c.out_channel});
+  if (downs_out) *downs_out = downs;
+  if (mid_out) *mid_out = mid;
+  if (ups_out) *ups_out = ups;
+  return all;
+}
+
+static std::map<std::string, std::vector<int64_t>> unet_param_shapes(const UNetCfg& c) {
+  std::map<std::string, std::vector<int64_t>> s;
+  const int64_t inner = c.inner;
+  s["noise_level_mlp.1.weight"] = {inner * 4, inner};
+  s["noise_level_mlp.1.bias"] = {inner * 4};
+  s["noise_level_mlp.3.weight"] = {inner, inner * 4};
+  s["noise_level_mlp.3.bias"] = {inner};
+  for (const auto& L : unet_layers(c, nullptr, nullptr, nullptr)) {
+    const std::string& n = L.name;
+    if (L.kind == 1) {
+      s[n + ".noise_func.noise_func.0.weight"] = {L.cout, inner};
+      s[n + ".noise_func.noise_func.0.bias"] = {L.cout};
+      s[n + ".block1.block.0.weight"] = {L.cin};
+      s[n + ".block1.block.0.bias"] = {L.cin};
+      s[n + ".block1.block.3.weight"] = {L.cout, L.cin, 3, 3};
+      s[n + ".block1.block.3.bias"] = {L.cout};
+      s[n + ".block2.block.0.weight"] = {L.cout};
+      s[n + ".block2.block.0.bias"] = {L.cout};
+      s[n + ".block2.block.3.weight"] = {L.cout, L.cout, 3, 3};
+      s[n + ".block2.block.3.bias"] = {L.cout};
+      if (L.cin != L.cout) {
+        s[n + ".res_conv.weight"] = {L.cout, L.cin, 1, 1};
+        s[n + ".res_conv.bias"] = {L.cout};
+      }
+    } else if (L.kind == 2 || L.kind == 3) {
+      s[n + ".conv.weight"] = {L.cout, L.cin, 3, 3};
+      s[n + ".conv.bias"] = {L.cout};
+    } else if (L.kind == 0) {
+      s[n + ".weight"] = {L.cout, L.cin, 3, 3};
+      s[n + ".bias"] = {L.cout};
+    } else {
+      s[n + ".block.0.weight"] = {L.cin};
+      s[n + ".block.0.bias"] = {L.cin};
+      s[n + ".block.3.weight"] = {L.cout, L.cin, 3, 3};
+      s[n + ".block.3.bias"] = {L.cout};
+    }
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------------
+struct Param { std::vector<int64_t> shape; std::vector<float> data; bool loaded = false; };
+struct Tensor { void* p = nullptr; int C = 0, H = 0, W = 0; float* stats = nullptr; int tiles = 0, n_tile = 0; };
+struct Op {
+  int cls;  // 0 conv_in, 1 gn, 2 conv3x3, 3 final, 4 other
+  double bytes, flops;
+  std::function<hipError_t(hipStream_t)> run;
+};
+struct ProfAcc { double ms = 0; int64_t n = 0; double bytes = 0, flops = 0; };
+
+struct RunState {  // fields patched into the plan's kernel arguments at launch time
+  const float* cond = nullptr;
+  float* x = nullptr;
+  const float* temb = nullptr;
+  int temb_per_b = 0;
+  int* t_dev = nullptr;
+  int final_mode = 0;
+  float* eps_out = nullptr;
+  uint64_t seed = 0;
+  int64_t row_offset = 0;
+};
+
+struct sddm_ctx {
+  int device = 0, dtype = DT_BF16;
+  bool configured = false;
+  // arch / diffusion
+  std::string arch_type, net_type, p_transition = "original";
+  int noise_time_step = 0;
+  int tr_mode = SDDM_TR_ORIGINAL, init_mode = 0;
+  int T = 0, num_samples = -1;
+  std::vector<float> tables;  // [14][T+1]
+  bool tables_dirty = true;
+  UNetCfg ucfg;
+  std::map<std::string, Param> params;
+  bool params_dirty = true;
+  // device state
+  Arena warena;      // weights + tables + temb table
+  size_t off_tables = 0, off_tdev = 0, off_temb_tab = 0;
+  std::map<std::string, size_t> woff;  // packed weight offsets
+  int SC = 0;
+  std::map<std::string, int> temb_off;  // per ResnetBlock offset in the projection vector
+  Arena aarena;      // activations of the current plan
+  int plan_B = -1;
+  std::vector<Op> ops;
+  size_t off_temb_fwd = 0, off_nl = 0;
+  RunState rs;
+  // profiling
+  bool prof = false;
+  std::vector<hipEvent_t> ev_pool;
+  std::vector<std::pair<int, int>> ev_used;  // (op cls, pool index of start event)
+  std::vector<double> ev_bytes, ev_flops;
+  std::map<int, ProfAcc> prof_acc;
+
+  const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
+  TransCoef coef() const {
+    TransCoef c;
+    c.betas = dtab(0); c.alphas = dtab(1); c.sqrt_alpha_bar = dtab(3); c.pnc = dtab(4);
+    c.sigma = dtab(5); c.sgamma = dtab(6); c.ssh = dtab(7); c.sqrt_delta = dtab(9);
+    c.c_xt = dtab(10); c.c_yt = dtab(11); c.c_epst = dtab(12); c.sde = dtab(13);
+    return c;
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// weight upload: pack every layer into the kernels' layouts in the compute dtype
+// ---------------------------------------------------------------------------------------------
+static int upload_weights(sddm_ctx* c) {
+  const int dt = c->dtype;
+  const size_t es = dtype_size(dt);
+  auto P = [&](const std::string& k) -> const Param& { return c->params.at(k); };
+  c->warena.reset();
+  c->woff.clear();
+  c->temb_off.clear();
+  Arena& A = c->warena;
+  struct Blob { size_t off; std::vector<char> bytes; };
+  std::vector<Blob> blobs;
+  auto add_f32 = [&](const std::string& name, const std::vector<float>& v) {
+    Blob b;
+    b.bytes.resize(v.size() * 4);
+    std::memcpy(b.bytes.data(), v.data(), b.bytes.size());
+    b.off = A.reserve(b.bytes.size());
+    c->woff[name] = b.off;
+    blobs.push_back(std::move(b));
+  };
+  // 3x3 conv weight [co][ci][3][3] -> [co_pad64][ci/32][9][32] (T)
+  auto add_conv3 = [&](const std::string& name, const Param& w) {
+    const int co = (int)w.shape[0], ci = (int)w.shape[1];
+    const int cop = (co + 63) / 64 * 64, nch = ci / 32;
+    Blob b;
+    b.bytes.assign((size_t)cop * ci * 9 * es, 0);
+    for (int o = 0; o < co; ++o)
+      for (int i = 0; i < ci; ++i)
+        for (int tap = 0; tap < 9; ++tap) {
+          const size_t dst = (((size_t)o * nch + i / 32) * 9 + tap) * 32 + (i % 32);
+          store_elem(b.bytes.data(), dst, w.data[((size_t)o * ci + i) * 9 + tap], dt);
+        }
+    b.off = A.reserve(b.bytes.size());
+    c->woff[name] = b.off;
+    blobs.push_back(std::move(b));
+  };
+  auto add_conv1 = [&](const std::string& name, const Param& w) {  // [co][ci] -> [co_pad64][ci]
+    const int co = (int)w.shape[0], ci = (int)w.shape[1];
+    const int cop = (co + 63) / 64 * 64;
+    Blob b;
+    b.bytes.assign((size_t)cop * ci * es, 0);
+    for (int o = 0; o < co; ++o)
+      for (int i = 0; i < ci; ++i) store_elem(b.bytes.data(), (size_t)o * ci + i, w.data[(size_t)o * ci + i], dt);
+    b.off = A.reserve(b.bytes.size());
+    c->woff[name] = b.off;
+    blobs.push_back(std::move(b));
+  };
+  const std::string pfx = "";
+  std::vector<float> pw, pb;
+  int sc = 0;
+  for (const auto& L : unet_layers(c->ucfg, nullptr, nullptr, nullptr)) {
+    const std::string& n = L.name;
+    if (L.kind == 0) {
+      add_f32(n + ".weight", P(n + ".weight").data);
+      add_f32(n + ".bias", P(n + ".bias").data);
+    } else if (L.kind == 1) {
+      add_f32(n + ".block1.gamma", P(n + ".block1.block.0.weight").data);
+      add_f32(n + ".block1.beta", P(n + ".block1.block.0.bias").data);
+      add_conv3(n + ".block1.w", P(n + ".block1.block.3.weight"));
+      add_f32(n + ".block1.b", P(n + ".block1.block.3.bias").data);
+      add_f32(n + ".block2.gamma", P(n + ".block2.block.0.weight").data);
+      add_f32(n + ".block2.beta", P(n + ".block2.block.0.bias").data);
+      add_conv3(n + ".block2.w", P(n + ".block2.block.3.weight"));
+      std::vector<float> b2 = P(n + ".block2.block.3.bias").data;
+      if (L.cin != L.cout) {
+        add_conv1(n + ".res.w", P(n + ".res_conv.weight"));
+        const auto& rb = P(n + ".res_conv.bias").data;
+        for (int i = 0; i < L.cout; ++i) b2[i] = b2[i] + rb[i];
+      }
+      add_f32(n + ".block2.b", b2);
+      const auto& fw = P(n + ".noise_func.noise_func.0.weight").data;
+      const auto& fb = P(n + ".noise_func.noise_func.0.bias").data;
+      pw.insert(pw.end(), fw.begin(), fw.end());
+      pb.insert(pb.end(), fb.begin(), fb.end());
+      c->temb_off[n] = sc;
+      sc += L.cout;
+    } else if (L.kind == 2 || L.kind == 3) {
+      add_conv3(n + ".w", P(n + ".conv.weight"));
+      add_f32(n + ".b", P(n + ".conv.bias").data);
+    } else {
+      add_f32(n + ".gamma", P(n + ".block.0.weight").data);
+      add_f32(n + ".beta", P(n + ".block.0.bias").data);
+      add_f32(n + ".w", P(n + ".block.3.weight").data);  // [1][C][3][3]
+      add_f32(n + ".b", P(n + ".block.3.bias").data);
+    }
+  }
+  add_f32("mlp.w1", P("noise_level_mlp.1.weight").data);
+  add_f32("mlp.b1", P("noise_level_mlp.1.bias").data);
+  add_f32("mlp.w2", P("noise_level_mlp.3.weight").data);
+  add_f32("mlp.b2", P("noise_level_mlp.3.bias").data);
+  add_f32("proj.w", pw);
+  add_f32("proj.b", pb);
+  {  // PositionalEncoding.embedding_vector (UNetModified2.py:53-55), fp32 ops as torch
+    const int half = c->ucfg.inner / 2;
+    std::vector<float> ev(half);
+    for (int k = 0; k < half; ++k) {
+      const float e = (-(float)k * 4.0f) / (float)half;
+      ev[k] = 1e4f * std::pow(10.0f, e);
+    }
+    add_f32("emb_vec", ev);
+  }
+  c->SC = sc;
+  c->off_tables = A.reserve(sizeof(float) * 14 * (c->T + 1));
+  c->off_tdev = A.reserve(64);
+  c->off_temb_tab = A.reserve(sizeof(float) * (size_t)(c->T + 1) * sc);
+  SDDM_HIP_CHECK(A.commit());
+  for (const auto& b : blobs) SDDM_HIP_CHECK(hipMemcpy(A.base + b.off, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice));
+  c->params_dirty = false;
+  c->tables_dirty = true;
+  c->plan_B = -1;  // plans hold weight pointers
+  return SDDM_OK;
+}
+
+static int upload_tables(sddm_ctx* c) {
+  SDDM_HIP_CHECK(hipMemcpy(c->warena.base + c->off_tables, c->tables.data(), sizeof(float) * c->tables.size(),
+                           hipMemcpyHostToDevice));
+  c->tables_dirty = false;
+  return SDDM_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// plan: the launch sequence of one UNetModified2 step for batch B
+// ---------------------------------------------------------------------------------------------
+static int choose_conv_cfg(int dt, ConvArgs& a, ConvCfg& cfg, bool s2) {
+  const int pix = a.Ho * a.Wo;
+  const int nb_pref = (a.Cout % 64 == 0) ? 64 : 32;
+  const int mb_pref = pix >= 2048 ? 128 : 64;
+  const int nbs[2] = {nb_pref, 32};
+  const int mbs[2] = {mb_pref, 64};
+  for (int ni = 0; ni < 2; ++ni)
+    for (int mi = 0; mi < 2; ++mi) {
+      cfg.stride2 = s2 ? 1 : 0;
+      cfg.nblk = nbs[ni];
+      cfg.mblk = mbs[mi];
+      a.TW = std::min(a.Wo, cfg.mblk);
+      a.TR = std::min(cfg.mblk / a.TW, a.Ho);
+      a.tiles_x = a.Wo / a.TW;
+      a.n_tiles = a.tiles_x * (a.Ho / a.TR);
+      if (conv3x3_lds_bytes(dt, cfg, a) <= 160 * 1024) return 0;
+    }
+  return 1;
+}
+
+static int build_plan(sddm_ctx* c, int B) {
+  const int dt = c->dtype;
+  const size_t es = dtype_size(dt);
+  const UNetCfg& u = c->ucfg;
+  const int N = c->num_samples, W = u.seg, S = u.stride;
+  const int F = (N - W) / S + 1;
+  c->ops.clear();
+  c->aarena.reset();
+  c->plan_B = -1;
+  Arena& A = c->aarena;
+
+  // ---- pass 1: symbolic program + buffer reservations ----
+  struct TRes { size_t p, st; int C, H, W, tiles, n_tile; };
+  std::vector<TRes> tres;
+  auto new_tensor = [&](int C, int H, int Wd, int tiles, int n_tile) -> int {
+    TRes t;
+    t.p = A.reserve((size_t)B * H * Wd * C * es);
+    t.st = A.reserve(sizeof(float) * (size_t)B * tiles * C * 2);
+    t.C = C; t.H = H; t.W = Wd; t.tiles = tiles; t.n_tile = n_tile;
+    tres.push_back(t);
+    return (int)tres.size() - 1;
+  };
+  struct GNRes { size_t sc, sh; };
+  std::vector<GNRes> gres;
+  auto new_gn = [&](int C) -> int {
+    gres.push_back({A.reserve(sizeof(float) * B * C), A.reserve(sizeof(float) * B * C)});
+    return (int)gres.size() - 1;
+  };
+  c->off_temb_fwd = A.reserve(sizeof(float) * (size_t)B * std::max(c->SC, 1));
+  c->off_nl = A.reserve(sizeof(float) * B);
+
+  enum { ST_CONVIN, ST_GN, ST_CONV, ST_FINAL };
+  struct Step {
+    int type = 0;
+    std::string w;          // weight-name prefix
+    std::string rb;         // ResnetBlock name (temb offset / res weights), "" if none
+    int srcA = -1, srcB = -1, gn = -1, out = -1;
+    int s2 = 0, up = 0, res_mode = 0, rawA = -1, rawB = -1, cout = 0;
+    bool temb = false;
+  };
+  std::vector<Step> prog;
+  auto geom = [&](int Ho, int Wo, int cout, bool s2, int& tiles, int& n_tile) -> bool {
+    ConvArgs a{}; a.Ho = Ho; a.Wo = Wo; a.Cout = cout; a.res_mode = 2;  // worst-case LDS
+    ConvCfg cfg;
+    if (choose_conv_cfg(dt, a, cfg, s2)) return false;
+    tiles = a.n_tiles; n_tile = a.TR * a.TW;
+    return true;
+  };
+  const int TRin = 2;
+  if (F % TRin) FAIL(SDDM_ERR_SHAPE, "n_frames %d not even", F);
+  const int t0 = new_tensor(u.inner, F, W, F / TRin, TRin * W);
+  { Step st; st.type = ST_CONVIN; st.out = t0; prog.push_back(st); }
+
+  auto res_block = [&](const std::string& n, int xa, int xb, int cin, int cout) -> int {
+    const int H = tres[xa].H, Wd = tres[xa].W;
+    int tiles, nt;
+    if (!geom(H, Wd, cout, false, tiles, nt)) return -1;
+    const int g1 = new_gn(cin);
+    { Step st; st.type = ST_GN; st.w = n + ".block1"; st.srcA = xa; st.srcB = xb; st.gn = g1; prog.push_back(st); }
+    const int h = new_tensor(cout, H, Wd, tiles, nt);
+    { Step st; st.type = ST_CONV; st.w = n + ".block1"; st.rb = n; st.srcA = xa; st.srcB = xb; st.gn = g1;
+      st.out = h; st.cout = cout; st.temb = true; prog.push_back(st); }
+    const int g2 = new_gn(cout);
+    { Step st; st.type = ST_GN; st.w = n + ".block2"; st.srcA = h; st.gn = g2; prog.push_back(st); }
+    const int o = new_tensor(cout, H, Wd, tiles, nt);
+    { Step st; st.type = ST_CONV; st.w = n + ".block2"; st.rb = n; st.srcA = h; st.gn = g2; st.out = o;
+      st.cout = cout; st.res_mode = cin != cout ? 2 : 1; st.rawA = xa; st.rawB = xb; prog.push_back(st); }
+    return o;
+  };
+  std::vector<LayerDesc> downs, mid, ups;
+  unet_layers(u, &downs, &mid, &ups);
+  std::vector<int> feats{t0};
+  int cur = t0;
+  for (size_t i = 1; i < downs.size(); ++i) {
+    const LayerDesc& L = downs[i];
+    if (L.kind == 1) {
+      cur = res_block(L.name, cur, -1, L.cin, L.cout);
+    } else {
+      if (tres[cur].H % 2 || tres[cur].W % 2) FAIL(SDDM_ERR_SHAPE, "odd size before %s", L.name.c_str());
+      const int H = tres[cur].H / 2, Wd = tres[cur].W / 2;
+      int tiles, nt;
+      if (!geom(H, Wd, L.cout, true, tiles, nt)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+      const int o = new_tensor(L.cout, H, Wd, tiles, nt);
+      Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.s2 = 1; st.cout = L.cout;
+      prog.push_back(st);
+      cur = o;
+    }
+    if (cur < 0) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+    feats.push_back(cur);
+  }
+  for (const LayerDesc& L : mid) {
+    cur = res_block(L.name, cur, -1, L.cin, L.cout);
+    if (cur < 0) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+  }
+  for (const LayerDesc& L : ups) {
+    if (L.kind == 1) {
+      const int skip = feats.back();
+      feats.pop_back();
+      if (tres[skip].H != tres[cur].H || tres[skip].W != tres[cur].W)
+        FAIL(SDDM_ERR_SHAPE, "skip/upsample size mismatch at %s (torch.cat would raise)", L.name.c_str());
+      cur = res_block(L.name, cur, skip, L.cin, L.cout);
+      if (cur < 0) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+    } else {
+      const int H = tres[cur].H * 2, Wd = tres[cur].W * 2;
+      int tiles, nt;
+      if (!geom(H, Wd, L.cout, false, tiles, nt)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+      const int o = new_tensor(L.cout, H, Wd, tiles, nt);
+      Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.up = 1; st.cout = L.cout;
+      prog.push_back(st);
+      cur = o;
+    }
+  }
+  const int gf = new_gn(tres[cur].C);
+  { Step st; st.type = ST_GN; st.w = "final_conv"; st.srcA = cur; st.gn = gf; prog.push_back(st); }
+  { Step st; st.type = ST_FINAL; st.srcA = cur; st.gn = gf; prog.push_back(st); }
+  SDDM_HIP_CHECK(A.commit());
+
+  // ---- pass 2: materialise kernel arguments ----
+  auto TT = [&](int i) {
+    Tensor t;
+    if (i < 0) return t;
+    const TRes& r = tres[i];
+    t.p = A.base + r.p; t.stats = A.at<float>(r.st); t.C = r.C; t.H = r.H; t.W = r.W;
+    t.tiles = r.tiles; t.n_tile = r.n_tile;
+    return t;
+  };
+  auto WF = [&](const std::string& k) { return c->warena.at<float>(c->woff.at(k)); };
+  auto WV = [&](const std::string& k) { return (const void*)(c->warena.base + c->woff.at(k)); };
+  sddm_ctx* ctx = c;
+  for (const Step& st : prog) {
+    if (st.type == ST_CONVIN) {
+      ConvInArgs a{};
+      a.N = N; a.F = F; a.W = W; a.S = S; a.Cout = u.inner;
+      a.w = WF("downs.0.weight"); a.bias = WF("downs.0.bias");
+      const Tensor o = TT(st.out);
+      a.out = o.p; a.stats = o.stats; a.TR = TRin;
+      const double bytes = (double)B * N * 4 * 2 + (double)B * F * W * u.inner * es;
+      const double flops = 2.0 * B * F * W * u.inner * 18;
+      c->ops.push_back({0, bytes, flops, [ctx, a, dt, B](hipStream_t s) {
+                          ConvInArgs x = a;
+                          x.cond = ctx->rs.cond; x.x = ctx->rs.x; x.t_dev = ctx->rs.t_dev;
+                          return launch_conv_in(dt, x, B, s);
+                        }});
+    } else if (st.type == ST_GN) {
+      GNArgs g{};
+      const Tensor ta = TT(st.srcA), tb = TT(st.srcB);
+      g.a = {ta.stats, ta.C, ta.tiles, ta.n_tile};
+      g.b = {tb.stats, tb.C, tb.tiles, tb.n_tile};
+      g.gamma = WF(st.w + ".gamma"); g.beta = WF(st.w + ".beta");
+      g.G = u.groups; g.eps = 1e-5f; g.B = B;
+      if ((ta.C + tb.C) % u.groups)
+        FAIL(SDDM_ERR_SHAPE, "GroupNorm(%d, %d): channels not divisible by groups", u.groups, ta.C + tb.C);
+      g.scale = A.at<float>(gres[st.gn].sc); g.shift = A.at<float>(gres[st.gn].sh);
+      const double bytes = (double)B * (ta.tiles * ta.C + tb.tiles * tb.C) * 8;
+      c->ops.push_back({1, bytes, 0.0, [g](hipStream_t s) { return launch_gn_finalize(g, s); }});
+    } else if (st.type == ST_CONV) {
+      ConvArgs a{};
+      const Tensor sa = TT(st.srcA), sb = TT(st.srcB), o = TT(st.out);
+      a.srcA = sa.p; a.srcB = sb.p; a.CA = sa.C; a.CB = sb.C;
+      a.Hi = sa.H; a.Wi = sa.W; a.Ho = o.H; a.Wo = o.W; a.upsample = st.up;
+      a.Cout = st.cout; a.out = o.p; a.stats = o.stats;
+      if (st.gn >= 0) { a.gn_scale = A.at<float>(gres[st.gn].sc); a.gn_shift = A.at<float>(gres[st.gn].sh); }
+      a.wgt = WV(st.w + ".w"); a.bias = WF(st.w + ".b");
+      a.res_mode = st.res_mode;
+      const int Cin = a.CA + a.CB;
+      double bytes = (double)B * a.Hi * a.Wi * Cin * es + (double)B * a.Ho * a.Wo * a.Cout * es +
+                     (double)a.Cout * 9 * Cin * es;
+      double flops = 2.0 * B * a.Ho * a.Wo * a.Cout * 9.0 * Cin;
+      if (st.res_mode == 1) {
+        a.res_src = TT(st.rawA).p;
+        bytes += (double)B * a.Ho * a.Wo * a.Cout * es;
+      } else if (st.res_mode == 2) {
+        const Tensor ra = TT(st.rawA), rb = TT(st.rawB);
+        a.rawA = ra.p; a.rawB = rb.p; a.RCA = ra.C; a.RCB = rb.C;
+        a.res_wgt = WV(st.rb + ".res.w");
+        if ((ra.C + rb.C) % 32) FAIL(SDDM_ERR_SHAPE, "%s.res_conv: channels must be multiples of 32", st.rb.c_str());
+        bytes += (double)B * a.Ho * a.Wo * (ra.C + rb.C) * es + (double)a.Cout * (ra.C + rb.C) * es;
+        flops += 2.0 * B * a.Ho * a.Wo * a.Cout * (double)(ra.C + rb.C);
+      }
+      ConvCfg cfg;
+      {  // same (worst-case LDS) choice as pass 1, so the stats tiling matches the tensor
+        ConvArgs probe = a;
+        probe.res_mode = 2;
+        if (choose_conv_cfg(dt, probe, cfg, st.s2)) FAIL(SDDM_ERR_SHAPE, "no conv tile fits LDS for %s", st.w.c_str());
+        a.TR = probe.TR; a.TW = probe.TW; a.tiles_x = probe.tiles_x; a.n_tiles = probe.n_tiles;
+        if (a.n_tiles != o.tiles || a.TR * a.TW != o.n_tile) FAIL(SDDM_ERR_STATE, "tile mismatch for %s", st.w.c_str());
+      }
+      if (Cin % 32 || a.Cout % 32) FAIL(SDDM_ERR_SHAPE, "%s: channels must be multiples of 32", st.w.c_str());
+      const bool temb = st.temb;
+      const int toff = temb ? c->temb_off.at(st.rb) : 0;
+      c->ops.push_back({2, bytes, flops, [ctx, a, cfg, dt, B, temb, toff](hipStream_t s) {
+                          ConvArgs x = a;
+                          if (temb) {
+                            x.temb = ctx->rs.temb + toff;
+                            x.temb_ld = ctx->SC;
+                            x.temb_per_b = ctx->rs.temb_per_b;
+                            x.t_dev = ctx->rs.t_dev;
+                          }
+                          return launch_conv3x3(dt, cfg, x, B, s);
+                        }});
+    } else {
+      FinalArgs f{};
+      const Tensor src = TT(st.srcA);
+      f.src = src.p; f.C = src.C;
+      f.gn_scale = A.at<float>(gres[st.gn].sc); f.gn_shift = A.at<float>(gres[st.gn].sh);
+      f.w = WF("final_conv.w");
+      f.bias = c->params.at("final_conv.block.3.bias").data[0];
+      f.N = N; f.F = F; f.W = W; f.S = S; f.FT = 2;
+      if (F % f.FT || W % S) FAIL(SDDM_ERR_SHAPE, "final tile: frames %d, segment %d/%d", F, W, S);
+      f.co = c->coef();
+      const double bytes = (double)B * F * W * src.C * es + (double)B * N * 4 * 3;
+      const double flops = 2.0 * B * F * W * src.C * 9;
+      c->ops.push_back({3, bytes, flops, [ctx, f, dt, B](hipStream_t s) {
+                          FinalArgs x = f;
+                          x.mode = ctx->rs.final_mode; x.eps_out = ctx->rs.eps_out;
+                          x.x = ctx->rs.x; x.cond = ctx->rs.cond; x.t_dev = ctx->rs.t_dev;
+                          x.seed = ctx->rs.seed; x.row_offset = ctx->rs.row_offset;
+                          return launch_final(dt, x, B, s);
+                        }});
+    }
+  }
+  c->plan_B = B;
+  return SDDM_OK;
+}
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+static int ensure_ready(sddm_ctx* c) {
+  if (!c || !c->configured) FAIL(SDDM_ERR_STATE, "context not configured");
+  if (c->net_type.empty()) FAIL(SDDM_ERR_STATE, "context has no network (diffusion-only)");
+  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  for (const auto& kv : c->params)
+    if (!kv.second.loaded) FAIL(SDDM_ERR_STATE, "parameter %s not loaded", kv.first.c_str());
+  if (c->params_dirty) {
+    const int r = upload_weights(c);
+    if (r) return r;
+  }
+  if (c->tables_dirty) {
+    const int r = upload_tables(c);
+    if (r) return r;
+  }
+  return SDDM_OK;
+}
+
+static int run_ops(sddm_ctx* c, hipStream_t s) {
+  for (const Op& op : c->ops) {
+    const bool timed = c->prof && (size_t)(c->ev_used.size() * 2 + 2) <= c->ev_pool.size();
+    int e0 = 0;
+    if (timed) {
+      e0 = (int)c->ev_used.size() * 2;
+      SDDM_HIP_CHECK(hipEventRecord(c->ev_pool[e0], s));
+    }
+    const hipError_t e = op.run(s);
+    if (e != hipSuccess) FAIL(SDDM_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+    if (timed) {
+      SDDM_HIP_CHECK(hipEventRecord(c->ev_pool[e0 + 1], s));
+      c->ev_used.push_back({op.cls, e0});
+      c->ev_bytes.push_back(op.bytes);
+      c->ev_flops.push_back(op.flops);
+    }
+  }
+  return SDDM_OK;
+}
+
+extern "C" {
+
+int sddm_abi_version(void) { return SDDM_ABI_VERSION; }
+const char* sddm_last_error(void) { return g_last_error.c_str(); }
+
+int sddm_create(int device, int compute_dtype, sddm_ctx** out) {
+  if (!out) FAIL(SDDM_ERR_INVALID_ARG, "out is NULL");
+  if (compute_dtype < 0 || compute_dtype > 2) FAIL(SDDM_ERR_INVALID_ARG, "bad dtype %d", compute_dtype);
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+    FAIL(SDDM_ERR_HIP, "no HIP device %d (count %d)", device, n);
+  sddm_ctx* c = new sddm_ctx();
+  c->device = device;
+  c->dtype = compute_dtype;
+  *out = c;
+  return SDDM_OK;
+}
+
+void sddm_destroy(sddm_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
+  c->aarena.reset();
+  c->warena.reset();
+  delete c;
+}
+
+int sddm_schedule(const char* schedule, int n_timestep, double linear_start, double linear_end, float* out) {
+  if (!schedule || !out || n_timestep < 1) FAIL(SDDM_ERR_INVALID_ARG, "bad schedule arguments");
+  if (compute_schedule(schedule, n_timestep, linear_start, linear_end, out))
+    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "schedule '%s'", schedule);
+  return SDDM_OK;
+}
+
+int sddm_configure(sddm_ctx* c, const char* json) {
+  if (!c || !json) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
+  Json cfg;
+  try {
+    cfg = Json::parse(json);
+  } catch (const std::exception& e) {
+    FAIL(SDDM_ERR_INVALID_ARG, "config JSON: %s", e.what());
+  }
+  const Json& arch = cfg.at("arch");
+  const Json& diff = cfg.at("diffusion");
+  const Json& net = cfg.at("network");
+  c->arch_type = arch.string("type", "SDDM");
+  const Json& aa = arch.at("args");
+  const std::string nc = aa.string("noise_condition", "sqrt_alpha_bar");
+  if (nc != "sqrt_alpha_bar" && nc != "time_step") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "noise_condition '%s'", nc.c_str());
+  c->noise_time_step = nc == "time_step";
+  if (c->arch_type == "SDDM") {
+    const std::string pt = aa.string("p_transition", "original");
+    const std::string qt = aa.string("q_transition", "original");
+    if (pt == "original") { c->tr_mode = SDDM_TR_ORIGINAL; c->init_mode = 0; }
+    else if (pt == "condition_in") { c->tr_mode = SDDM_TR_ORIGINAL; c->init_mode = 4; }
+    else if (pt == "sr3") { c->tr_mode = SDDM_TR_SR3; c->init_mode = 1; }
+    else if (pt == "supportive") { c->tr_mode = SDDM_TR_SUPPORTIVE; c->init_mode = 2; }
+    else if (pt == "conditional") { c->tr_mode = SDDM_TR_CONDITIONAL; c->init_mode = 3; }
+    else FAIL(SDDM_ERR_NOT_IMPLEMENTED, "p_transition '%s' (model.py:20-23)", pt.c_str());
+    if (qt != "original" && qt != "conditional") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "q_transition '%s'", qt.c_str());
+    c->p_transition = pt;
+  } else if (c->arch_type == "SDDM_spectrogram") {
+    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "arch SDDM_spectrogram (DiffWave/WaveGrad path) is not built in this library version");
+  } else {
+    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "arch type '%s'", c->arch_type.c_str());
+  }
+  if (diff.string("type", "GaussianDiffusion") != "GaussianDiffusion")
+    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "diffusion type '%s'", diff.string("type", "").c_str());
+  const Json& da = diff.at("args");
+  const std::string sched = da.string("schedule", "linear");
+  const int T = (int)da.number("n_timestep", 1000);
+  const double ls = da.number("linear_start", 1e-4), le = da.number("linear_end", 2e-2);
+  if (T < 1) FAIL(SDDM_ERR_INVALID_ARG, "n_timestep %d", T);
+  std::vector<float> tabs((size_t)14 * (T + 1));
+  if (compute_schedule(sched, T, ls, le, tabs.data())) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "schedule '%s' (diffusion.py:84)", sched.c_str());
+  c->net_type = net.string("type", "");
+  if (c->net_type.empty()) {  // diffusion-only context: transitions / initial state
+    c->T = T;
+    c->tables.swap(tabs);
+    c->tables_dirty = true;
+    c->params.clear();
+    c->plan_B = -1;
+    c->aarena.reset();
+    c->warena.reset();
+    c->configured = true;
+    return SDDM_OK;
+  }
+  if (c->net_type != "UNetModified2") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "network type '%s'", c->net_type.c_str());
+  const Json& na = net.at("args");
+  UNetCfg u;
+  u.in_channel = (int)na.number("in_channel", 2);
+  u.out_channel = (int)na.number("out_channel", 1);
+  u.inner = (int)na.number("inner_channel", 32);
+  u.groups = (int)na.number("norm_groups", 32);
+  u.mults = na.ints("channel_mults", {1, 2, 3, 4, 5});
+  u.res_blocks = (int)na.number("res_blocks", 3);
+  u.dropout = na.number("dropout", 0.0);
+  u.seg = (int)na.number("segment_len", 128);
+  u.stride = (int)na.number("segment_stride", 64);
+  const int Ns = (int)cfg.number("num_samples", (double)na.number("num_samples", -1));
+  if (u.in_channel != 2 || u.out_channel != 1)
+    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "UNetModified2 with in_channel %d / out_channel %d", u.in_channel, u.out_channel);
+  if (u.inner > 128 || u.inner % 32) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "inner_channel %d (multiples of 32 up to 128)", u.inner);
+  if (Ns <= u.seg || (Ns - u.seg) % u.stride) FAIL(SDDM_ERR_SHAPE, "num_samples %d: (n - %d) %% %d != 0 (UNetModified2.py:13)", Ns, u.seg, u.stride);
+  const int F = (Ns - u.seg) / u.stride + 1;
+  const int div = 1 << (int)u.mults.size();
+  if (F % div || u.seg % div) FAIL(SDDM_ERR_SHAPE, "n_frames %d and segment_len %d must be multiples of %d", F, u.seg, div);
+  if (u.seg % u.stride) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "segment_len %% segment_stride != 0");
+  c->T = T;
+  c->tables.swap(tabs);
+  c->tables_dirty = true;
+  c->ucfg = u;
+  c->num_samples = Ns;
+  c->params.clear();
+  for (const auto& kv : unet_param_shapes(u)) {
+    Param p;
+    p.shape = kv.second;
+    c->params[kv.first] = p;
+  }
+  c->params_dirty = true;
+  c->plan_B = -1;
+  c->aarena.reset();
+  c->warena.reset();
+  c->configured = true;
+  return SDDM_OK;
+}
+
+int sddm_load_param(sddm_ctx* c, const char* key_c, const void* host_ptr, const int64_t* shape, int ndim,
+                    int src_dtype) {
+  if (!c || !c->configured) FAIL(SDDM_ERR_STATE, "context not configured");
+  if (!key_c || !host_ptr || (ndim > 0 && !shape)) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
+  std::string key = key_c;
+  if (key.rfind("module.", 0) == 0) key = key.substr(7);
+  int64_t n = 1;
+  for (int i = 0; i < ndim; ++i) n *= shape[i];
+  auto read = [&](std::vector<float>& dst) -> int {
+    dst.resize((size_t)n);
+    if (src_dtype == DT_F32) std::memcpy(dst.data(), host_ptr, sizeof(float) * n);
+    else if (src_dtype == DT_BF16) {
+      for (int64_t i = 0; i < n; ++i) {
+        uint32_t u = (uint32_t)((const uint16_t*)host_ptr)[i] << 16;
+        std::memcpy(&dst[i], &u, 4);
+      }
+    } else if (src_dtype == DT_F16) {
+      for (int64_t i = 0; i < n; ++i) dst[i] = (float)((const _Float16*)host_ptr)[i];
+    } else {
+      return 1;
+    }
+    return 0;
+  };
+  if (key.rfind("diffusion.", 0) == 0) {
+    const std::string name = key.substr(10);
+    for (int k = 0; k < 14; ++k)
+      if (name == kTableNames[k]) {
+        if (ndim != 1 || shape[0] != c->T + 1)
+          FAIL(SDDM_ERR_SHAPE, "%s: expected [%d]", key.c_str(), c->T + 1);
+        std::vector<float> v;
+        if (read(v)) FAIL(SDDM_ERR_INVALID_ARG, "bad src dtype %d", src_dtype);
+        std::memcpy(c->tables.data() + (size_t)k * (c->T + 1), v.data(), sizeof(float) * v.size());
+        c->tables_dirty = true;
+        return SDDM_OK;
+      }
+    FAIL(SDDM_ERR_INVALID_ARG, "unexpected key %s", key.c_str());
+  }
+  if (key.rfind("noise_estimate_model.", 0) == 0) key = key.substr(21);
+  auto it = c->params.find(key);
+  if (it == c->params.end()) FAIL(SDDM_ERR_INVALID_ARG, "unexpected key %s", key_c);
+  Param& p = it->second;
+  if ((int)p.shape.size() != ndim) FAIL(SDDM_ERR_SHAPE, "%s: rank %d != %d", key_c, ndim, (int)p.shape.size());
+  for (int i = 0; i < ndim; ++i)
+    if (p.shape[i] != shape[i]) FAIL(SDDM_ERR_SHAPE, "%s: shape mismatch in dim %d", key_c, i);
+  if (read(p.data)) FAIL(SDDM_ERR_INVALID_ARG, "bad src dtype %d", src_dtype);
+  p.loaded = true;
+  c->params_dirty = true;
+  return SDDM_OK;
+}
+
+int sddm_missing_params(sddm_ctx* c, int64_t* n_missing) {
+  if (!c || !n_missing) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
+  int64_t m = 0;
+  for (const auto& kv : c->params) m += kv.second.loaded ? 0 : 1;
+  *n_missing = m;
+  return SDDM_OK;
+}
+
+static int prepare_plan(sddm_ctx* c, int64_t B, int64_t N) {
+  if (N != c->num_samples)
+    FAIL(SDDM_ERR_SHAPE, "condition has %lld samples, network built for num_samples=%d", (long long)N, c->num_samples);
+  if (B < 1 || B > 65535) FAIL(SDDM_ERR_INVALID_ARG, "batch %lld", (long long)B);
+  if (c->plan_B != (int)B) return build_plan(c, (int)B);
+  return SDDM_OK;
+}
+
+int sddm_sample(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed, int64_t row_offset,
+                float* out, void* stream) {
+  int r = ensure_ready(c);
+  if (r) return r;
+  if (!cond || !out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  r = prepare_plan(c, B, N);
+  if (r) return r;
+  hipStream_t s = (hipStream_t)stream;
+  const int T = c->T;
+  int* t_dev = c->warena.at<int>(c->off_tdev);
+  float* temb_tab = c->warena.at<float>(c->off_temb_tab);
+  // noise-level embeddings of every t (same for all rows: model.py:108)
+  EmbedArgs e{};
+  e.table = c->dtab(3); e.time_step_mode = c->noise_time_step; e.R = T + 1; e.dim = c->ucfg.inner;
+  e.emb_vec = c->warena.at<float>(c->woff.at("emb_vec"));
+  e.w1 = c->warena.at<float>(c->woff.at("mlp.w1")); e.b1 = c->warena.at<float>(c->woff.at("mlp.b1"));
+  e.w2 = c->warena.at<float>(c->woff.at("mlp.w2")); e.b2 = c->warena.at<float>(c->woff.at("mlp.b2"));
+  e.pw = c->warena.at<float>(c->woff.at("proj.w")); e.pb = c->warena.at<float>(c->woff.at("proj.b"));
+  e.SC = c->SC; e.out = temb_tab;
+  SDDM_HIP_CHECK(launch_embed(e, s));
+  InitArgs ia{};
+  ia.mode = c->init_mode; ia.cond = cond; ia.out = out; ia.total = B * N; ia.N = N; ia.T = T;
+  ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset;
+  SDDM_HIP_CHECK(launch_init_state(ia, s));
+  SDDM_HIP_CHECK(launch_set_int(t_dev, T + 1, s));
+  c->rs.cond = cond; c->rs.x = out; c->rs.temb = temb_tab; c->rs.temb_per_b = 0; c->rs.t_dev = t_dev;
+  c->rs.final_mode = c->tr_mode; c->rs.eps_out = nullptr; c->rs.seed = seed; c->rs.row_offset = row_offset;
+  for (int t = T; t >= 1; --t) {
+    r = run_ops(c, s);
+    if (r) return r;
+  }
+  return SDDM_OK;
+}
+
+int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const float* noise_level, int64_t B,
+                         int64_t N, float* eps_out, void* stream) {
+  int r = ensure_ready(c);
+  if (r) return r;
+  if (!cond || !x_t || !noise_level || !eps_out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  r = prepare_plan(c, B, N);
+  if (r) return r;
+  hipStream_t s = (hipStream_t)stream;
+  float* temb = c->aarena.at<float>(c->off_temb_fwd);
+  EmbedArgs e{};
+  e.noise_levels = noise_level; e.R = (int)B; e.dim = c->ucfg.inner;
+  e.emb_vec = c->warena.at<float>(c->woff.at("emb_vec"));
+  e.w1 = c->warena.at<float>(c->woff.at("mlp.w1")); e.b1 = c->warena.at<float>(c->woff.at("mlp.b1"));
+  e.w2 = c->warena.at<float>(c->woff.at("mlp.w2")); e.b2 = c->warena.at<float>(c->woff.at("mlp.b2"));
+  e.pw = c->warena.at<float>(c->woff.at("proj.w")); e.pb = c->warena.at<float>(c->woff.at("proj.b"));
+  e.SC = c->SC; e.out = temb;
+  SDDM_HIP_CHECK(launch_embed(e, s));
+  c->rs.cond = cond; c->rs.x = const_cast<float*>(x_t); c->rs.temb = temb; c->rs.temb_per_b = 1;
+  c->rs.t_dev = nullptr; c->rs.final_mode = -1; c->rs.eps_out = eps_out; c->rs.seed = 0; c->rs.row_offset = 0;
+  return run_ops(c, s);
+}
+
+int sddm_transition(sddm_ctx* c, int mode, const float* x_t, const float* eps, const float* cond, int t, int64_t B,
+                    int64_t N, uint64_t seed, int64_t row_offset, float* out, void* stream) {
+  if (!c || !c->configured) FAIL(SDDM_ERR_STATE, "context not configured");
+  if (mode < 0 || mode > 4) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "transition mode %d", mode);
+  if (t < 1 || t > c->T) FAIL(SDDM_ERR_INVALID_ARG, "t=%d outside [1, %d]", t, c->T);
+  if (!x_t || !eps || !out || (mode >= 2 && mode <= 3 && !cond)) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  if (!c->warena.base) {  // tables only (no network needed for a transition)
+    c->warena.reset();
+    c->off_tables = c->warena.reserve(sizeof(float) * 14 * (c->T + 1));
+    c->off_tdev = c->warena.reserve(64);
+    SDDM_HIP_CHECK(c->warena.commit());
+    c->params_dirty = true;
+    c->tables_dirty = true;
+  }
+  if (c->tables_dirty) {
+    const int r = upload_tables(c);
+    if (r) return r;
+  }
+  TransArgs a{};
+  a.mode = mode; a.x_t = x_t; a.eps = eps; a.cond = cond; a.out = out; a.total = B * N; a.N = N; a.t = t;
+  a.co = c->coef(); a.seed = seed; a.row_offset = row_offset;
+  SDDM_HIP_CHECK(launch_transition(a, (hipStream_t)stream));
+  return SDDM_OK;
+}
+
+int sddm_initial_state(sddm_ctx* c, int mode, const float* cond, int64_t B, int64_t N, uint64_t seed,
+                       int64_t row_offset, float* out, void* stream) {
+  if (!c || !c->configured) FAIL(SDDM_ERR_STATE, "context not configured");
+  if (mode < 0 || mode > 4) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "init mode %d", mode);
+  if (!out || (mode >= 2 && !cond)) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  if (!c->warena.base) {
+    c->warena.reset();
+    c->off_tables = c->warena.reserve(sizeof(float) * 14 * (c->T + 1));
+    c->off_tdev = c->warena.reserve(64);
+    SDDM_HIP_CHECK(c->warena.commit());
+    c->params_dirty = true;
+    c->tables_dirty = true;
+  }
+  if (c->tables_dirty) {
+    const int r = upload_tables(c);
+    if (r) return r;
+  }
+  InitArgs ia{};
+  ia.mode = mode; ia.cond = cond; ia.out = out; ia.total = B * N; ia.N = N; ia.T = c->T;
+  ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset;
+  SDDM_HIP_CHECK(launch_init_state(ia, (hipStream_t)stream));
+  return SDDM_OK;
+}
+
+int sddm_profile_enable(sddm_ctx* c, int enable) {
+  if (!c) FAIL(SDDM_ERR_INVALID_ARG, "NULL ctx");
+  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  c->prof = enable != 0;
+  c->ev_used.clear(); c->ev_bytes.clear(); c->ev_flops.clear(); c->prof_acc.clear();
+  if (c->prof && c->ev_pool.empty()) {
+    c->ev_pool.resize(20000);
+    for (auto& e : c->ev_pool) SDDM_HIP_CHECK(hipEventCreate(&e));
+  }
+  return SDDM_OK;
+}
+
+int sddm_profile_read(sddm_ctx* c, const char* kernel_class, double* avg_ms, int64_t* launches,
+                      double* bytes_per_launch, double* flops_per_launch) {
+  if (!c || !kernel_class) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
+  const std::string k = kernel_class;
+  const int cls = k == "conv_in" ? 0 : k == "gn_finalize" ? 1 : k == "conv3x3" ? 2 : k == "final" ? 3 : -1;
+  if (cls < 0) FAIL(SDDM_ERR_INVALID_ARG, "kernel class %s", kernel_class);
+  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  double ms = 0, bytes = 0, flops = 0;
+  int64_t n = 0;
+  for (size_t i = 0; i < c->ev_used.size(); ++i) {
+    if (c->ev_used[i].first != cls) continue;
+    const int e0 = c->ev_used[i].second;
+    SDDM_HIP_CHECK(hipEventSynchronize(c->ev_pool[e0 + 1]));
+    float m = 0;
+    SDDM_HIP_CHECK(hipEventElapsedTime(&m, c->ev_pool[e0], c->ev_pool[e0 + 1]));
+    ms += m; bytes += c->ev_bytes[i]; flops += c->ev_flops[i]; ++n;
+  }
+  if (avg_ms) *avg_ms = n ? ms / n : 0.0;
+  if (launches) *launches = n;
+  if (bytes_per_launch) *bytes_per_launch = n ? bytes / n : 0.0;
+  if (flops_per_launch) *flops_per_launch = n ? flops / n : 0.0;
+  return SDDM_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,172 @@
+"""ctypes binding of libsddm_hip.so (C ABI: include/sddm_hip.h).
+
+This is the only way the Python facade reaches the hot path.  There is no CPU or torch
+fallback: if the library is missing, or no HIP device is visible, calls raise.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsddm_hip.so")
+
+OK, ERR_NOT_IMPLEMENTED, ERR_INVALID_ARG, ERR_SHAPE, ERR_HIP, ERR_STATE = range(6)
+F32, BF16, F16 = 0, 1, 2
+TR_ORIGINAL, TR_SR3, TR_SUPPORTIVE, TR_CONDITIONAL, TR_CONDITION_IN = range(5)
+DTYPES = {"float32": F32, "fp32": F32, "f32": F32, "bfloat16": BF16, "bf16": BF16,
+          "float16": F16, "fp16": F16, "f16": F16}
+TRANSITIONS = {"original": TR_ORIGINAL, "condition_in": TR_CONDITION_IN, "sr3": TR_SR3,
+               "supportive": TR_SUPPORTIVE, "conditional": TR_CONDITIONAL}
+TABLE_NAMES = ("betas", "alphas", "alpha_bar", "sqrt_alpha_bar", "predicted_noise_coeff", "sigma",
+               "supportive_gamma", "supportive_sigma_hat", "m", "sqrt_delta", "c_xt", "c_yt", "c_epst",
+               "sqrt_delta_estimated")
+EXPORTS = ("sddm_abi_version", "sddm_last_error", "sddm_create", "sddm_destroy", "sddm_configure",
+           "sddm_load_param", "sddm_missing_params", "sddm_sample", "sddm_network_forward",
+           "sddm_transition", "sddm_initial_state", "sddm_schedule", "sddm_profile_enable",
+           "sddm_profile_read")
+
+_lib = None
+
+
+def lib():
+    """Load libsddm_hip.so (fails loudly when it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} not built: run __graft_entry__.build() or "
+                               "python speech-denoising-diffusion-model-2_amd/sddm_hip/build.py")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i64, u64, c_int = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64, ctypes.c_int
+        L.sddm_abi_version.restype = c_int
+        L.sddm_last_error.restype = ctypes.c_char_p
+        L.sddm_create.argtypes = [c_int, c_int, ctypes.POINTER(vp)]
+        L.sddm_destroy.argtypes = [vp]
+        L.sddm_destroy.restype = None
+        L.sddm_configure.argtypes = [vp, ctypes.c_char_p]
+        L.sddm_load_param.argtypes = [vp, ctypes.c_char_p, vp, ctypes.POINTER(i64), c_int, c_int]
+        L.sddm_missing_params.argtypes = [vp, ctypes.POINTER(i64)]
+        L.sddm_sample.argtypes = [vp, vp, i64, i64, u64, i64, vp, vp]
+        L.sddm_network_forward.argtypes = [vp, vp, vp, vp, i64, i64, vp, vp]
+        L.sddm_transition.argtypes = [vp, c_int, vp, vp, vp, c_int, i64, i64, u64, i64, vp, vp]
+        L.sddm_initial_state.argtypes = [vp, c_int, vp, i64, i64, u64, i64, vp, vp]
+        L.sddm_schedule.argtypes = [ctypes.c_char_p, c_int, ctypes.c_double, ctypes.c_double, vp]
+        L.sddm_profile_enable.argtypes = [vp, c_int]
+        L.sddm_profile_read.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_double)]
+        for name in EXPORTS:
+            if name not in ("sddm_last_error", "sddm_destroy", "sddm_abi_version"):
+                getattr(L, name).restype = c_int
+        _lib = L
+    return _lib
+
+
+class SddmError(RuntimeError):
+    pass
+
+
+def check(status):
+    """Map a status code to the exception type the reference raises for the same condition."""
+    if status == OK:
+        return
+    msg = lib().sddm_last_error().decode(errors="replace")
+    if status == ERR_NOT_IMPLEMENTED:
+        raise NotImplementedError(msg)
+    if status == ERR_SHAPE:
+        raise AssertionError(msg)
+    if status == ERR_INVALID_ARG:
+        raise ValueError(msg)
+    raise SddmError(f"sddm status {status}: {msg}")
+
+
+def schedule(schedule="linear", n_timestep=1000, linear_start=1e-4, linear_end=2e-2):
+    """The 14 GaussianDiffusion buffers (host computation in the library, no GPU needed)."""
+    out = np.empty((14, int(n_timestep) + 1), dtype=np.float32)
+    check(lib().sddm_schedule(str(schedule).encode(), int(n_timestep), float(linear_start),
+                              float(linear_end), out.ctypes.data))
+    return dict(zip(TABLE_NAMES, out))
+
+
+def _ptr(t):
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream(torch, device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Context:
+    """One configured sampler on one HIP device (owns weights, tables, workspace)."""
+
+    def __init__(self, config, device=0, compute_dtype="float32"):
+        self.device = int(device)
+        self.dtype = DTYPES[str(compute_dtype)]
+        h = ctypes.c_void_p()
+        check(lib().sddm_create(self.device, self.dtype, ctypes.byref(h)))
+        self._h = h
+        check(lib().sddm_configure(self._h, json.dumps(config).encode()))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sddm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def load_param(self, key, array):
+        a = np.ascontiguousarray(np.asarray(array, dtype=np.float32))
+        shape = (ctypes.c_int64 * max(a.ndim, 1))(*a.shape)
+        check(lib().sddm_load_param(self._h, key.encode(), a.ctypes.data, shape, a.ndim, F32))
+
+    def load_state_dict(self, state):
+        for k, v in state.items():
+            if hasattr(v, "detach"):
+                v = v.detach().float().cpu().numpy()
+            self.load_param(k, v)
+
+    def missing(self):
+        n = ctypes.c_int64()
+        check(lib().sddm_missing_params(self._h, ctypes.byref(n)))
+        return n.value
+
+    # the torch tensors below are device tensors (fp32, contiguous) on self.device
+    def sample(self, cond, out, seed, row_offset=0):
+        import torch
+        B, N = cond.shape[0], cond.shape[-1]
+        check(lib().sddm_sample(self._h, _ptr(cond), B, N, int(seed) & (2 ** 64 - 1), int(row_offset),
+                                _ptr(out), _stream(torch, cond.device)))
+
+    def network_forward(self, cond, x_t, noise_level, eps_out):
+        import torch
+        B, N = cond.shape[0], cond.shape[-1]
+        check(lib().sddm_network_forward(self._h, _ptr(cond), _ptr(x_t), _ptr(noise_level), B, N,
+                                         _ptr(eps_out), _stream(torch, cond.device)))
+
+    def transition(self, mode, x_t, eps, cond, t, out, seed, row_offset=0):
+        import torch
+        B, N = x_t.shape[0], x_t.numel() // x_t.shape[0]
+        check(lib().sddm_transition(self._h, int(mode), _ptr(x_t), _ptr(eps), _ptr(cond), int(t), B, N,
+                                    int(seed) & (2 ** 64 - 1), int(row_offset), _ptr(out),
+                                    _stream(torch, x_t.device)))
+
+    def initial_state(self, mode, cond, out, seed, row_offset=0):
+        import torch
+        B, N = out.shape[0], out.numel() // out.shape[0]
+        check(lib().sddm_initial_state(self._h, int(mode), _ptr(cond), B, N, int(seed) & (2 ** 64 - 1),
+                                       int(row_offset), _ptr(out), _stream(torch, out.device)))
+
+    def profile(self, enable=True):
+        check(lib().sddm_profile_enable(self._h, 1 if enable else 0))
+
+    def profile_read(self, kernel_class):
+        ms, b, f = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        n = ctypes.c_int64()
+        check(lib().sddm_profile_read(self._h, kernel_class.encode(), ctypes.byref(ms), ctypes.byref(n),
+                                      ctypes.byref(b), ctypes.byref(f)))
+        return dict(avg_ms=ms.value, launches=n.value, bytes_per_launch=b.value, flops_per_launch=f.value)
