@@ -80,6 +80,12 @@ int sddm_missing_params(sddm_ctx* ctx, int64_t* n_missing);
 int sddm_sample(sddm_ctx* ctx, const float* cond, int64_t B, int64_t N, uint64_t seed,
                 int64_t row_offset, float* out, void* stream);
 
+/* SDDM.infer(condition, continuous=True) (model/model.py:79-103): as sddm_sample, and after the
+ * step at t, whenever t % sample_inter == 0, x_{t-1} is copied to the next slot of `record`
+ * ([T / sample_inter][B][N] fp32 device).  sample_inter = 1 | (T // 100) (model.py:72). */
+int sddm_sample_continuous(sddm_ctx* ctx, const float* cond, int64_t B, int64_t N, uint64_t seed,
+                           int64_t row_offset, float* out, float* record, int sample_inter, void* stream);
+
 /* Replaces one noise_estimate_model(condition, x_t, noise_level) call (model.py:110):
  * noise_level: [B] fp32 device.  eps_out: [B, 1, N] fp32 device. */
 int sddm_network_forward(sddm_ctx* ctx, const float* cond, const float* x_t,

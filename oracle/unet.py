@@ -99,8 +99,9 @@ def conv2d(x, w, b, stride=1):
     """nn.Conv2d(k=3, pad=1, stride) or k=1 as tap-shifted GEMMs."""
     B, C, H, W = x.shape
     co, ci, kh, kw = w.shape
-    if kh == 1:
-        out = np.einsum("oc,bchw->bohw", w[:, :, 0, 0], x, optimize=True)
+    if kh == 1:   # per batch row, so results do not depend on how rows are batched / sharded
+        w2 = np.ascontiguousarray(w[:, :, 0, 0])
+        out = np.stack([(w2 @ x[i].reshape(C, H * W)).reshape(co, H, W) for i in range(B)])
         return (out + b[None, :, None, None]).astype(np.float32)
     Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
     wm = np.ascontiguousarray(w.transpose(0, 2, 3, 1).reshape(co, 9 * C))   # k = (tap, ci)
@@ -117,7 +118,8 @@ def conv2d(x, w, b, stride=1):
 
 
 def linear(x, w, b):
-    return (x @ w.T + b).astype(np.float32)
+    """nn.Linear, row by row (batch-invariant rounding)."""
+    return np.stack([w @ xi + b for xi in x]).astype(np.float32)
 
 
 def noise_level_embedding(P, noise_level, inner):

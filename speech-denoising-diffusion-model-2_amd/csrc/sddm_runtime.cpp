@@ -858,8 +858,22 @@ static int prepare_plan(sddm_ctx* c, int64_t B, int64_t N) {
   return SDDM_OK;
 }
 
+static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed, int64_t row_offset,
+                       float* out, float* record, int sample_inter, void* stream);
+
 int sddm_sample(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed, int64_t row_offset,
                 float* out, void* stream) {
+  return sample_impl(c, cond, B, N, seed, row_offset, out, nullptr, 0, stream);
+}
+
+int sddm_sample_continuous(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed,
+                           int64_t row_offset, float* out, float* record, int sample_inter, void* stream) {
+  if (!record || sample_inter < 1) FAIL(SDDM_ERR_INVALID_ARG, "record buffer / sample_inter");
+  return sample_impl(c, cond, B, N, seed, row_offset, out, record, sample_inter, stream);
+}
+
+static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed, int64_t row_offset,
+                       float* out, float* record, int sample_inter, void* stream) {
   int r = ensure_ready(c);
   if (r) return r;
   if (!cond || !out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
@@ -885,9 +899,14 @@ int sddm_sample(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t s
   SDDM_HIP_CHECK(launch_set_int(t_dev, T + 1, s));
   c->rs.cond = cond; c->rs.x = out; c->rs.temb = temb_tab; c->rs.temb_per_b = 0; c->rs.t_dev = t_dev;
   c->rs.final_mode = c->tr_mode; c->rs.eps_out = nullptr; c->rs.seed = seed; c->rs.row_offset = row_offset;
+  int64_t nrec = 0;
   for (int t = T; t >= 1; --t) {
     r = run_ops(c, s);
     if (r) return r;
+    if (record && t % sample_inter == 0) {  // model.py:100-101: keep x_{t-1} when t % inter == 0
+      SDDM_HIP_CHECK(hipMemcpyAsync(record + nrec * B * N, out, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
+      ++nrec;
+    }
   }
   return SDDM_OK;
 }

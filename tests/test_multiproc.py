@@ -1,0 +1,60 @@
+"""Multi-rank sharding (CPU, gloo, world_size 2).
+
+bench.py / the sharded sampler give rank r the contiguous rows [r*B, (r+1)*B) with
+row_offset = r*B and gather the outputs with one all-gather at the end.  Because
+the noise stream is keyed by the global row, the gathered result must equal a single-process run
+of all rows bit for bit.  Checked here with the oracle sampler as the per-rank worker and the same
+gather layout (all_gather into a [world*B] tensor) over gloo.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _worker(rank, world, port, out_path):
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "speech-denoising-diffusion-model-2_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import sampler, unet
+    from _helpers import tables_from_golden, unet_arch, unet_params
+    from sddm_hip.synth import noisy_speech
+    N, B = 2112, 1
+    P, arch = unet_params(N), unet_arch(N)
+    tab = tables_from_golden("linear_3_0.0001_0.05")
+    cond = noisy_speech(B * world, N, seed=1234)[rank * B:(rank + 1) * B]
+    x = sampler.infer(lambda c, xx, nl: unet.forward(P, arch, c, xx, nl), tab, cond, "condition_in", seed=7,
+                      row_offset=rank * B)
+    gathered = [torch.empty(B, 1, N) for _ in range(world)]
+    dist.all_gather(gathered, torch.from_numpy(x))
+    if rank == 0:
+        np.save(out_path, torch.cat(gathered).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gather_equals_single_run(tmp_path):
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out_path = str(tmp_path / "gathered.npy")
+    mp.spawn(_worker, args=(2, port, out_path), nprocs=2, join=True)
+    from oracle import sampler, unet
+    from _helpers import tables_from_golden, unet_arch, unet_params
+    from sddm_hip.synth import noisy_speech
+    N = 2112
+    P, arch = unet_params(N), unet_arch(N)
+    full = sampler.infer(lambda c, xx, nl: unet.forward(P, arch, c, xx, nl),
+                         tables_from_golden("linear_3_0.0001_0.05"), noisy_speech(2, N, seed=1234),
+                         "condition_in", seed=7)
+    assert np.array_equal(np.load(out_path), full)
