@@ -114,6 +114,8 @@ int sddm_schedule(const char* schedule, int n_timestep, double linear_start, dou
 int sddm_profile_enable(sddm_ctx* ctx, int enable);
 int sddm_profile_read(sddm_ctx* ctx, const char* kernel_class, double* avg_ms, int64_t* launches,
                       double* bytes_per_launch, double* flops_per_launch);
+/* Per-op breakdown of the timed launches as a JSON array written into buf. */
+int sddm_profile_ops(sddm_ctx* ctx, char* buf, int64_t buflen);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,175 @@
+// MFMA fragment helpers shared by the convolution kernels (gfx950, wave64).
+//
+// 16x16 tiles with A = weights (rows = output channels) and B = pixels (cols): lane l holds
+// A[co = l & 15][k = 8 (l >> 4) + j] and B[k = 8 (l >> 4) + j][px = l & 15] (j = 0..7); the fp32
+// accumulator holds D[co = 4 (l >> 4) + i][px = l & 15].  For T = float the 8 channels of a
+// lane group are consumed by 8 MFMA 16x16x4 instructions (element j -> k-set {j, 8+j, 16+j,
+// 24+j}); any k permutation shared by A and B gives the same dot product.
+#pragma once
+#include "sddm_common.h"
+
+namespace sddm {
+
+template <typename T> struct Frag;
+template <> struct Frag<bf16_t> { bf16x8 v; };
+template <> struct Frag<f16_t> { f16x8 v; };
+template <> struct Frag<float> { f32x4 lo, hi; };
+
+template <typename T> __device__ __forceinline__ Frag<T> load_frag(const char* p);
+template <> __device__ __forceinline__ Frag<bf16_t> load_frag<bf16_t>(const char* p) { return {*(const bf16x8*)p}; }
+template <> __device__ __forceinline__ Frag<f16_t> load_frag<f16_t>(const char* p) { return {*(const f16x8*)p}; }
+template <> __device__ __forceinline__ Frag<float> load_frag<float>(const char* p) {
+  return {*(const f32x4*)p, *(const f32x4*)(p + 16)};
+}
+
+__device__ __forceinline__ void mfma_frag(f32x4& acc, const Frag<bf16_t>& a, const Frag<bf16_t>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mfma_frag(f32x4& acc, const Frag<f16_t>& a, const Frag<f16_t>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(a.v, b.v, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mfma_frag(f32x4& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.lo[j], b.lo[j], acc, 0, 0, 0);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.hi[j], b.hi[j], acc, 0, 0, 0);
+}
+
+template <typename T> struct Mfma {
+  static __device__ __forceinline__ void run(f32x4& acc, const char* pa, const char* pb) {
+    mfma_frag(acc, load_frag<T>(pa), load_frag<T>(pb));
+  }
+};
+
+// GroupNorm affine + SiLU on one 16-byte vector (16 / sizeof(T) channels), re-rounded to T.
+template <typename T>
+__device__ __forceinline__ f32x4 transform_vec(f32x4 raw, const float* sc, const float* sh, bool gn) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(VE)));
+  if (!gn) return raw;
+  vec v = __builtin_bit_cast(vec, raw);
+#pragma unroll
+  for (int j = 0; j < VE; ++j) v[j] = from_f32<T>(silu(to_f32<T>(v[j]) * sc[j] + sh[j]));
+  return __builtin_bit_cast(f32x4, v);
+}
+
+template <typename T>
+__device__ __forceinline__ void transform16(char* dst, const char* src, const float* sc, const float* sh, bool gn) {
+  *(f32x4*)dst = transform_vec<T>(*(const f32x4*)src, sc, sh, gn);
+}
+
+// store 4 consecutive channels (one accumulator) as T
+template <typename T> __device__ __forceinline__ void store4(T* p, float a, float b, float c, float d);
+template <> __device__ __forceinline__ void store4<float>(float* p, float a, float b, float c, float d) {
+  *(f32x4*)p = f32x4{a, b, c, d};
+}
+template <> __device__ __forceinline__ void store4<bf16_t>(bf16_t* p, float a, float b, float c, float d) {
+  *(bf16x4*)p = bf16x4{(bf16_t)a, (bf16_t)b, (bf16_t)c, (bf16_t)d};
+}
+template <> __device__ __forceinline__ void store4<f16_t>(f16_t* p, float a, float b, float c, float d) {
+  *(f16x4*)p = f16x4{(f16_t)a, (f16_t)b, (f16_t)c, (f16_t)d};
+}
+template <typename T> __device__ __forceinline__ f32x4 load4(const T* p);
+template <> __device__ __forceinline__ f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
+template <> __device__ __forceinline__ f32x4 load4<bf16_t>(const bf16_t* p) {
+  const bf16x4 v = *(const bf16x4*)p;
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+template <> __device__ __forceinline__ f32x4 load4<f16_t>(const f16_t* p) {
+  const f16x4 v = *(const f16x4*)p;
+  return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+}
+template <typename T> __device__ __forceinline__ float round_t(float v) { return to_f32<T>(from_f32<T>(v)); }
+
+}  // namespace sddm
+
+namespace sddm {
+
+// ---------------------------------------------------------------------------------------------
+// GroupNorm finalize fused into a consumer's prologue (nn.GroupNorm, UNetModified2.py:117).
+// Producers leave per-tile (sum, M2 about the tile mean) of every channel; the consumer block
+// combines them for its image b with Chan's formula in fp64 (two deterministic passes) and
+// writes per-channel scale / shift = gamma*rstd, beta - mean*gamma*rstd into LDS.
+// Groups never straddle the A|B concat boundary (checked on the host).
+// ---------------------------------------------------------------------------------------------
+struct GNFuse {
+  const float* statsA; int tilesA, ntileA;
+  const float* statsB; int tilesB, ntileB;
+  const float* gamma; const float* beta;
+  int G; float eps;
+};
+
+__device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
+  const int C = CA + CB, cpg = C / f.G;
+  const int tpg = blockDim.x / f.G;               // threads per group (power of two, <= 64)
+  const int g = threadIdx.x / tpg, sub = threadIdx.x - g * tpg;
+  if (g >= f.G) return;
+  const int c0 = g * cpg;
+  const bool fromA = c0 < CA;
+  const float* st = fromA ? f.statsA : f.statsB;
+  const int tiles = fromA ? f.tilesA : f.tilesB;
+  const int ntile = fromA ? f.ntileA : f.ntileB;
+  const int Cs = fromA ? CA : CB;
+  const int cs0 = fromA ? c0 : c0 - CA;
+  const int items = cpg * tiles;
+  const float* base = st + (size_t)b * tiles * Cs * 2;
+  double s = 0.0;
+  for (int i = sub; i < items; i += tpg) {
+    const int c = i / tiles, t = i - c * tiles;
+    s += (double)base[((size_t)t * Cs + cs0 + c) * 2];
+  }
+  for (int o = 1; o < tpg; o <<= 1) s += __shfl_xor(s, o);
+  const double n_tot = (double)items * ntile;
+  const double mean = s / n_tot;
+  double m2 = 0.0;
+  for (int i = sub; i < items; i += tpg) {
+    const int c = i / tiles, t = i - c * tiles;
+    const float* e = base + ((size_t)t * Cs + cs0 + c) * 2;
+    const double d = (double)e[0] / ntile - mean;
+    m2 += (double)e[1] + (double)ntile * d * d;
+  }
+  for (int o = 1; o < tpg; o <<= 1) m2 += __shfl_xor(m2, o);
+  const double rstd = 1.0 / sqrt(m2 / n_tot + (double)f.eps);
+  for (int c = sub; c < cpg; c += tpg) {
+    const double scale = (double)f.gamma[c0 + c] * rstd;
+    sc[c0 + c] = (float)scale;
+    sh[c0 + c] = (float)((double)f.beta[c0 + c] - mean * scale);
+  }
+}
+
+}  // namespace sddm
+
+namespace sddm {
+// =============================================================================================
+// Per-channel tile statistics from an fp32 LDS tile [npix][ld] (values already rounded to the
+// storage type).  Writes (sum, M2 about the tile mean) for channels [0, nch).
+// =============================================================================================
+__device__ __forceinline__ void tile_channel_stats(const float* tile, int ld, int npix, int nch, float* dst,
+                                   int dst_stride) {
+  // threads split as (channel, part); parts combine through shuffles within a wave group
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int parts = max(1, min(nthr / max(nch, 1), 16));
+  // round parts down to power of two
+  int p2 = 1;
+  while (p2 * 2 <= parts) p2 *= 2;
+  const int c = tid / p2, part = tid % p2;
+  float s = 0.f;
+  const bool act = c < nch;
+  if (act)
+    for (int p = part; p < npix; p += p2) s += tile[p * ld + c];
+  for (int o = 1; o < p2; o <<= 1) s += __shfl_xor(s, o);
+  const float mean = s / (float)npix;
+  float m2 = 0.f;
+  if (act)
+    for (int p = part; p < npix; p += p2) {
+      const float d = tile[p * ld + c] - mean;
+      m2 += d * d;
+    }
+  for (int o = 1; o < p2; o <<= 1) m2 += __shfl_xor(m2, o);
+  if (act && part == 0) {
+    dst[c * dst_stride] = s;
+    dst[c * dst_stride + 1] = m2;
+  }
+}
+
+}  // namespace sddm

@@ -46,13 +46,18 @@ struct ConvInArgs {
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s);
 
 // ---- MFMA implicit-GEMM 3x3 convolution (Block / Downsample / Upsample / ResnetBlock) ----
+struct GNFuse;
 struct ConvArgs {
   const void* srcA; const void* srcB; int CA, CB;  // virtual channel concat (UNetModified2.py:263)
   int Hi, Wi;                 // stored source dims
   int Ho, Wo;                 // output dims
   int upsample;               // stride-1 kernel reads a nearest-2x upsampled source (UNetModified2.py:96-100)
   int TR, TW, tiles_x, n_tiles;
-  const float* gn_scale; const float* gn_shift;    // [B][CA+CB] or null (no GN / SiLU prologue)
+  // GroupNorm + SiLU prologue (Block, UNetModified2.py:116-120): the producer's per-tile statistics
+  // are finalized in the consumer (gamma == null: no GN / SiLU)
+  const float* gstA; int gtilesA, gntileA;
+  const float* gstB; int gtilesB, gntileB;
+  const float* gamma; const float* beta; int groups; float eps;
   const void* wgt;            // packed [Cout_pad][Cin/32][9][32] (T)
   const float* bias;          // [Cout]
   const float* temb; int temb_ld; const int* t_dev; int temb_per_b;  // + temb row (ResnetBlock.noise_func)
@@ -64,9 +69,13 @@ struct ConvArgs {
   void* out;                  // [B][Ho][Wo][Cout]
   float* stats;               // [B][n_tiles][Cout][2] (sum, M2 about tile mean) or null
 };
-struct ConvCfg { int stride2; int nblk; int mblk; };
+struct ConvCfg { int stride2; int kw; int fp; int nblk; };   // K-split waves, pixel frags per wave
 hipError_t launch_conv3x3(int dtype, const ConvCfg& cfg, const ConvArgs& a, int B, hipStream_t s);
 size_t conv3x3_lds_bytes(int dtype, const ConvCfg& cfg, const ConvArgs& a);
+
+// ---- row-streaming 3x3 convolution for segment widths 64 / 128 (conv_strip.hip) ----
+hipError_t launch_conv_strip(int dtype, int nblk, int SR, const ConvArgs& a, int B, hipStream_t s);
+size_t conv_strip_lds_bytes(int dtype, int nblk, const ConvArgs& a);
 
 // ---- final Block(C -> 1) + overlapAdd + p_transition (UNetModified2.py:235,267-268; diffusion.py:164-223) ----
 struct TransCoef {            // device pointers to the GaussianDiffusion buffers [T+1]
@@ -76,7 +85,8 @@ struct TransCoef {            // device pointers to the GaussianDiffusion buffer
 };
 struct FinalArgs {
   const void* src; int C;     // [B][F][W][C] (T)
-  const float* gn_scale; const float* gn_shift;  // [B][C]
+  const float* gst; int gtiles, gntile;          // producer tile statistics (final_conv GroupNorm)
+  const float* gamma; const float* beta; int groups; float eps;
   const float* w; float bias; // [C][3][3] fp32 (out_channel = 1)
   int N, F, W, S, FT;
   int mode;                   // -1: write eps (network forward); else sddm_transition mode

@@ -10,11 +10,11 @@
 // the MFMA K dimension (tap, channel) reads 16-byte vectors straight from LDS.
 #include "sddm_common.h"
 #include "kernels.h"
+#include "conv_common.h"
 #include <algorithm>
 
 namespace sddm {
 
-static __device__ __forceinline__ int round16(int x) { return (x + 15) & ~15; }
 
 // =============================================================================================
 // Noise-level embedding: PositionalEncoding -> Linear -> Swish -> Linear -> Swish
@@ -126,38 +126,6 @@ hipError_t launch_gn_finalize(const GNArgs& a, hipStream_t s) {
 }
 
 // =============================================================================================
-// Per-channel tile statistics from an fp32 LDS tile [npix][ld] (values already rounded to the
-// storage type).  Writes (sum, M2 about the tile mean) for channels [0, nch).
-// =============================================================================================
-__device__ void tile_channel_stats(const float* tile, int ld, int npix, int nch, float* dst,
-                                   int dst_stride) {
-  // threads split as (channel, part); parts combine through shuffles within a wave group
-  const int tid = threadIdx.x, nthr = blockDim.x;
-  const int parts = max(1, min(nthr / max(nch, 1), 16));
-  // round parts down to power of two
-  int p2 = 1;
-  while (p2 * 2 <= parts) p2 *= 2;
-  const int c = tid / p2, part = tid % p2;
-  float s = 0.f;
-  const bool act = c < nch;
-  if (act)
-    for (int p = part; p < npix; p += p2) s += tile[p * ld + c];
-  for (int o = 1; o < p2; o <<= 1) s += __shfl_xor(s, o);
-  const float mean = s / (float)npix;
-  float m2 = 0.f;
-  if (act)
-    for (int p = part; p < npix; p += p2) {
-      const float d = tile[p * ld + c] - mean;
-      m2 += d * d;
-    }
-  for (int o = 1; o < p2; o <<= 1) m2 += __shfl_xor(m2, o);
-  if (act && part == 0) {
-    dst[c * dst_stride] = s;
-    dst[c * dst_stride + 1] = m2;
-  }
-}
-
-// =============================================================================================
 // conv_in: SignalToFrames on cond and x_t (idx[f,w] = S*f + w), channel concat, Conv2d(2, C, 3,
 // pad 1) + bias.  One thread per output pixel, TR frame rows per block.
 // =============================================================================================
@@ -213,280 +181,6 @@ hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s) 
   else if (dtype == DT_BF16) hipLaunchKernelGGL(conv_in_kernel<bf16_t>, grid, dim3(256), lds, s, a);
   else hipLaunchKernelGGL(conv_in_kernel<f16_t>, grid, dim3(256), lds, s, a);
   return hipGetLastError();
-}
-
-// =============================================================================================
-// MFMA implicit-GEMM 3x3 convolution.
-//   D[co][pixel] = sum_{tap, ci} W[co][tap][ci] * X[pixel + tap][ci]
-// A operand = weights (rows = output channels), B operand = input pixels (cols), so each lane's
-// accumulator holds 4 consecutive channels of one pixel (C/D layout: col = lane & 15,
-// row = 4 * (lane >> 4) + i).  The K loop walks 32-channel chunks; per chunk the block stages
-// the transformed halo tile and the weight slab in LDS.
-// Block = 4 waves stacked along pixels; wave tile = (FP*16 pixels) x (FC*16 channels).
-// =============================================================================================
-template <typename T> struct Mfma;
-template <> struct Mfma<bf16_t> {
-  typedef bf16x8 frag;
-  static __device__ __forceinline__ void run(f32x4& acc, const char* pa, const char* pb) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(const bf16x8*)pa, *(const bf16x8*)pb, acc, 0, 0, 0);
-  }
-};
-template <> struct Mfma<f16_t> {
-  static __device__ __forceinline__ void run(f32x4& acc, const char* pa, const char* pb) {
-    acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(*(const f16x8*)pa, *(const f16x8*)pb, acc, 0, 0, 0);
-  }
-};
-template <> struct Mfma<float> {
-  // 8 channels per lane group: MFMA j consumes element j (k-set {j, 8+j, 16+j, 24+j}).
-  static __device__ __forceinline__ void run(f32x4& acc, const char* pa, const char* pb) {
-    const f32x4 a0 = *(const f32x4*)pa, a1 = *(const f32x4*)(pa + 16);
-    const f32x4 b0 = *(const f32x4*)pb, b1 = *(const f32x4*)(pb + 16);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a0[j], b0[j], acc, 0, 0, 0);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], b1[j], acc, 0, 0, 0);
-  }
-};
-
-template <typename T>
-__device__ __forceinline__ void transform16(char* dst, const char* src, const float* sc, const float* sh,
-                                            bool gn) {
-  // 16 bytes = 16/sizeof(T) elements; GN affine + SiLU in fp32, re-round to T
-  constexpr int VE = 16 / (int)sizeof(T);
-  typedef T vec __attribute__((ext_vector_type(VE)));
-  vec v = *(const vec*)src;
-  if (gn) {
-#pragma unroll
-    for (int j = 0; j < VE; ++j) v[j] = from_f32<T>(silu(to_f32<T>(v[j]) * sc[j] + sh[j]));
-  }
-  *(vec*)dst = v;
-}
-
-template <int ES> struct LdsGeom {
-  static constexpr int CK = 32;
-  static constexpr int PIX = CK * ES + 16;       // bytes per halo pixel (16-B pad vs bank conflicts)
-  static constexpr int WROW = 9 * CK * ES + 16;  // bytes per output channel of a weight chunk
-  static constexpr int RROW = CK * ES + 16;      // bytes per output channel of a 1x1 chunk
-};
-
-template <typename T, bool S2, int FP, int FC>
-__global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
-  constexpr int WM = 4;
-  constexpr int ES = (int)sizeof(T);
-  typedef LdsGeom<ES> G;
-  constexpr int CK = G::CK, PIX = G::PIX, WROW = G::WROW, RROW = G::RROW;
-  constexpr int MBLK = WM * FP * 16, NBLK = FC * 16;
-  constexpr int UPP = CK * ES / 16;  // 16-byte units per pixel chunk
-  constexpr int VE = 16 / ES;
-  constexpr int LG = 8 * ES;         // bytes of one lane group's 8 channels
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tile = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NBLK;
-  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  const int y0 = ty * a.TR, x0 = tx * a.TW;
-  const int HR = S2 ? 2 * a.TR + 1 : a.TR + 2, HC = S2 ? 2 * a.TW + 1 : a.TW + 2;
-  const int Cin = a.CA + a.CB;
-  const bool gn = a.gn_scale != nullptr;
-  const bool res2 = a.res_mode == 2;
-
-  char* halo = smem;
-  char* wl = halo + round16(HR * HC * PIX);
-  char* raw = wl + NBLK * WROW;
-  char* rw = raw + (res2 ? MBLK * PIX : 0);
-  float* gsc = (float*)(rw + (res2 ? NBLK * RROW : 0));
-
-  const int npix_valid = a.TR * a.TW;
-  int pix_off[FP];
-#pragma unroll
-  for (int fp = 0; fp < FP; ++fp) {
-    int p = wave * FP * 16 + fp * 16 + (lane & 15);
-    if (p >= npix_valid) p = 0;
-    const int py = p / a.TW, px = p - py * a.TW;
-    pix_off[fp] = ((S2 ? 2 * py : py) * HC + (S2 ? 2 * px : px)) * PIX + (lane >> 4) * LG;
-  }
-  f32x4 acc[FP][FC];
-#pragma unroll
-  for (int i = 0; i < FP; ++i)
-#pragma unroll
-    for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const size_t img_in = (size_t)a.Hi * a.Wi;
-  const int nchunk = Cin / CK;
-  for (int ck = 0; ck < nchunk; ++ck) {
-    const int c0 = ck * CK;
-    const bool fromA = c0 < a.CA;
-    const T* src = fromA ? (const T*)a.srcA : (const T*)a.srcB;
-    const int Cs = fromA ? a.CA : a.CB;
-    const int cs0 = fromA ? c0 : c0 - a.CA;
-    __syncthreads();
-    if (gn && tid < CK) {
-      gsc[tid] = a.gn_scale[(size_t)b * Cin + c0 + tid];
-      gsc[CK + tid] = a.gn_shift[(size_t)b * Cin + c0 + tid];
-    }
-    // weight slab: rows n0..n0+NBLK, chunk ck, 9 taps x 32 channels (contiguous per row)
-    for (int u = tid; u < NBLK * 9 * UPP; u += 256) {
-      const int row = u / (9 * UPP), q = u - row * 9 * UPP;
-      const char* g = (const char*)a.wgt + (((size_t)(n0 + row) * nchunk + ck) * 9 * CK) * ES + q * 16;
-      *(f32x4*)(wl + row * WROW + q * 16) = *(const f32x4*)g;
-    }
-    if (gn) __syncthreads();  // gsc visible to the halo transform
-    for (int u = tid; u < HR * HC * UPP; u += 256) {
-      const int hp = u / UPP, q = u - hp * UPP;
-      const int hy = hp / HC, hx = hp - hy * HC;
-      int iy, ix;
-      bool ok;
-      if (S2) {
-        iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
-        ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
-      } else {
-        iy = y0 - 1 + hy; ix = x0 - 1 + hx;
-        ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
-        if (a.upsample) { iy >>= 1; ix >>= 1; }
-      }
-      char* dst = halo + hp * PIX + q * 16;
-      if (ok) {
-        const size_t pi = (size_t)b * img_in + (size_t)iy * a.Wi + ix;
-        transform16<T>(dst, (const char*)(src + pi * Cs + cs0) + q * 16, gsc + q * VE, gsc + CK + q * VE, gn);
-      } else {
-        *(f32x4*)dst = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    __syncthreads();
-    const char* wbase = wl + (lane & 15) * WROW + (lane >> 4) * LG;
-#pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      const int dy = tap / 3, dx = tap - dy * 3;
-      const int toff = (dy * HC + dx) * PIX;
-#pragma unroll
-      for (int fc = 0; fc < FC; ++fc)
-#pragma unroll
-        for (int fp = 0; fp < FP; ++fp)
-          Mfma<T>::run(acc[fp][fc], wbase + fc * 16 * WROW + tap * CK * ES, halo + pix_off[fp] + toff);
-    }
-  }
-  // ---- fused ResnetBlock.res_conv: 1x1 over the raw block input (K = RCA + RCB) ----
-  if (res2) {
-    const int rcin = a.RCA + a.RCB;
-    for (int c0 = 0; c0 < rcin; c0 += CK) {
-      const bool fromA = c0 < a.RCA;
-      const T* src = fromA ? (const T*)a.rawA : (const T*)a.rawB;
-      const int Cs = fromA ? a.RCA : a.RCB;
-      const int cs0 = fromA ? c0 : c0 - a.RCA;
-      __syncthreads();
-      for (int u = tid; u < NBLK * UPP; u += 256) {
-        const int row = u / UPP, q = u - row * UPP;
-        const char* g = (const char*)a.res_wgt + ((size_t)(n0 + row) * rcin + c0) * ES + q * 16;
-        *(f32x4*)(rw + row * RROW + q * 16) = *(const f32x4*)g;
-      }
-      for (int u = tid; u < MBLK * UPP; u += 256) {
-        const int p = u / UPP, q = u - p * UPP;
-        f32x4 v = {0.f, 0.f, 0.f, 0.f};
-        if (p < npix_valid) {
-          const int py = p / a.TW, px = p - py * a.TW;
-          const size_t pi = ((size_t)b * a.Ho + (y0 + py)) * a.Wo + (x0 + px);
-          v = *(const f32x4*)((const char*)(src + pi * Cs + cs0) + q * 16);
-        }
-        *(f32x4*)(raw + p * PIX + q * 16) = v;
-      }
-      __syncthreads();
-      const char* rbase = rw + (lane & 15) * RROW + (lane >> 4) * LG;
-#pragma unroll
-      for (int fc = 0; fc < FC; ++fc)
-#pragma unroll
-        for (int fp = 0; fp < FP; ++fp) {
-          const int p = wave * FP * 16 + fp * 16 + (lane & 15);
-          Mfma<T>::run(acc[fp][fc], rbase + fc * 16 * RROW, raw + p * PIX + (lane >> 4) * LG);
-        }
-    }
-  }
-  __syncthreads();
-  // ---- epilogue: bias + embedding + residual, round to T, stage in LDS ----
-  constexpr int OLD = NBLK + 1;
-  float* ot = (float*)smem;
-  const int t = a.t_dev ? *a.t_dev : 0;
-  const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t) * a.temb_ld : nullptr;
-#pragma unroll
-  for (int fp = 0; fp < FP; ++fp) {
-    const int p = wave * FP * 16 + fp * 16 + (lane & 15);
-    const bool pv = p < npix_valid;
-    const int py = p / a.TW, px = p - py * a.TW;
-    const size_t po = ((size_t)b * a.Ho + (y0 + py)) * a.Wo + (x0 + px);
-#pragma unroll
-    for (int fc = 0; fc < FC; ++fc) {
-      const int cl = fc * 16 + 4 * (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int co = n0 + cl + i;
-        float v = acc[fp][fc][i];
-        if (co < a.Cout) {
-          v += a.bias[co];
-          if (trow) v += trow[co];
-          if (a.res_mode == 1 && pv) v += to_f32<T>(((const T*)a.res_src)[po * a.Cout + co]);
-        }
-        ot[p * OLD + cl + i] = to_f32<T>(from_f32<T>(v));
-      }
-    }
-  }
-  __syncthreads();
-  // ---- store: each valid pixel writes its NBLK (<= Cout - n0) channels ----
-  const int nco = min(NBLK, a.Cout - n0);
-  for (int u = tid; u < npix_valid * nco; u += 256) {
-    const int p = u / nco, c = u - p * nco;
-    const int py = p / a.TW, px = p - py * a.TW;
-    const size_t po = ((size_t)b * a.Ho + (y0 + py)) * a.Wo + (x0 + px);
-    ((T*)a.out)[po * a.Cout + n0 + c] = from_f32<T>(ot[p * OLD + c]);
-  }
-  if (a.stats)
-    tile_channel_stats(ot, OLD, npix_valid, nco,
-                       a.stats + (((size_t)b * a.n_tiles + tile) * a.Cout + n0) * 2, 2);
-}
-
-template <typename T, bool S2, int FP, int FC>
-static size_t lds_bytes_t(const ConvArgs& a) {
-  typedef LdsGeom<(int)sizeof(T)> G;
-  constexpr int MBLK = 4 * FP * 16, NBLK = FC * 16;
-  const int HR = S2 ? 2 * a.TR + 1 : a.TR + 2, HC = S2 ? 2 * a.TW + 1 : a.TW + 2;
-  size_t main = ((size_t)HR * HC * G::PIX + 15) / 16 * 16 + (size_t)NBLK * G::WROW;
-  if (a.res_mode == 2) main += (size_t)MBLK * G::PIX + (size_t)NBLK * G::RROW;
-  main += 2 * G::CK * 4;
-  const size_t epi = (size_t)MBLK * (NBLK + 1) * 4;
-  return main > epi ? main : epi;
-}
-
-template <typename T, bool S2, int FP, int FC>
-static hipError_t launch_t(const ConvArgs& a, int B, hipStream_t s, size_t* lds_only) {
-  const size_t lds = lds_bytes_t<T, S2, FP, FC>(a);
-  if (lds_only) { *lds_only = lds; return hipSuccess; }
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  const int nz = (a.Cout + FC * 16 - 1) / (FC * 16);
-  hipLaunchKernelGGL((conv3x3_kernel<T, S2, FP, FC>), dim3(a.n_tiles, B, nz), dim3(256), lds, s, a);
-  return hipGetLastError();
-}
-
-template <typename T>
-static hipError_t dispatch_t(const ConvCfg& c, const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
-#define SDDM_CONV_CASE(S2V, FPV, FCV)                                                           \
-  if (c.stride2 == S2V && c.mblk == 64 * FPV && c.nblk == 16 * FCV)                             \
-    return launch_t<T, S2V, FPV, FCV>(a, B, s, lo);
-  SDDM_CONV_CASE(0, 1, 2) SDDM_CONV_CASE(0, 2, 2) SDDM_CONV_CASE(0, 1, 4) SDDM_CONV_CASE(0, 2, 4)
-  SDDM_CONV_CASE(1, 1, 2) SDDM_CONV_CASE(1, 2, 2) SDDM_CONV_CASE(1, 1, 4) SDDM_CONV_CASE(1, 2, 4)
-#undef SDDM_CONV_CASE
-  return hipErrorInvalidValue;
-}
-
-hipError_t launch_conv3x3(int dtype, const ConvCfg& cfg, const ConvArgs& a, int B, hipStream_t s) {
-  if (dtype == DT_F32) return dispatch_t<float>(cfg, a, B, s, nullptr);
-  if (dtype == DT_BF16) return dispatch_t<bf16_t>(cfg, a, B, s, nullptr);
-  return dispatch_t<f16_t>(cfg, a, B, s, nullptr);
-}
-
-size_t conv3x3_lds_bytes(int dtype, const ConvCfg& cfg, const ConvArgs& a) {
-  size_t lo = 0;
-  if (dtype == DT_F32) (void)dispatch_t<float>(cfg, a, 1, 0, &lo);
-  else if (dtype == DT_BF16) (void)dispatch_t<bf16_t>(cfg, a, 1, 0, &lo);
-  else (void)dispatch_t<f16_t>(cfg, a, 1, 0, &lo);
-  return lo;
 }
 
 // =============================================================================================
@@ -549,8 +243,12 @@ __global__ __launch_bounds__(256) void init_state_kernel(InitArgs a) {
 
 // =============================================================================================
 // Final Block (GN+SiLU -> Conv 3x3 C->1) + overlapAdd + transition, fused.  A block owns frames
-// [f0, f0+FT) and the samples [S*f0, S*(f0+FT)) (the last block also the tail up to N); it
-// recomputes the W/S-1 preceding frames it needs for the overlap-add.
+// [f0, f0+FT) and the samples [S*f0, S*(f0+FT)) (the last block also the tail up to N).
+//  phase 1: every input pixel of rows [f0-back-1, f0+FT] -> its 9 per-tap partial dot products
+//           P[tap] = sum_c w[c][tap] * silu(gn(x[c])) (each pixel transformed once), in LDS;
+//  phase 2: y[f][w] = bias + sum_taps P[tap][f+dy-1][w+dx-1] for frames [f0-back, f0+FT);
+//  phase 3: overlapAdd in ascending frame order (UNetModified2.py:37-39) and p_transition, four
+//           consecutive samples per thread (one Philox counter group).
 // =============================================================================================
 template <typename T>
 __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
@@ -559,43 +257,51 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   const int C = a.C, W = a.W, S = a.S, F = a.F;
   const int back = W / S - 1;                 // extra frames before f0 needed by the OLA
   const int YR = a.FT + back;                 // y rows: frames [f0-back, f0+FT)
-  const int IR = YR + 2, IC = W + 2;          // transformed input rows/cols
-  const int CL = C + 4;                       // padded channel stride (floats)
-  float* in = (float*)smem;                   // [IR][IC][CL]
-  float* wl = in + IR * IC * CL;              // [9][C]
-  float* y = wl + 9 * C;                      // [YR][W]
-  float* gs = y + YR * W;                     // [2][C]
-  for (int i = tid; i < C; i += blockDim.x) {
-    gs[i] = a.gn_scale[(size_t)b * C + i];
-    gs[C + i] = a.gn_shift[(size_t)b * C + i];
+  const int PR = YR + 2, PC = W + 2;          // partial-product rows / cols (zero halo cols)
+  float* P = (float*)smem;                    // [9][PR][PC]
+  float* y = P + 9 * PR * PC;                 // [YR][W]
+  float* wl = y + YR * W;                     // [C][9]
+  float* gs = wl + 9 * C;                     // [2][C]
+  {
+    const GNFuse gf{a.gst, a.gtiles, a.gntile, nullptr, 0, 0, a.gamma, a.beta, a.groups, a.eps};
+    gn_fused_prologue(gf, b, C, 0, gs, gs + C);
   }
-  for (int i = tid; i < 9 * C; i += blockDim.x) {
-    const int tap = i / C, c = i - tap * C;
-    wl[i] = a.w[c * 9 + tap];
-  }
+  for (int i = tid; i < 9 * C; i += blockDim.x) wl[i] = a.w[i];   // [c][tap] as Conv2d(C,1,3)
   __syncthreads();
   const T* src = (const T*)a.src + (size_t)b * F * W * C;
-  for (int u = tid; u < IR * IC * C; u += blockDim.x) {
-    const int c = u % C, pp = u / C, ix = pp % IC, iy = pp / IC;
-    const int f = f0 - back - 1 + iy, w = ix - 1;
-    float v = 0.f;
-    if (f >= 0 && f < F && w >= 0 && w < W)
-      v = silu(to_f32<T>(src[((size_t)f * W + w) * C + c]) * gs[c] + gs[C + c]);
-    in[(iy * IC + ix) * CL + c] = v;
+  const float* __restrict__ wg = a.w;
+  constexpr int VE = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(VE)));
+  for (int pp = tid; pp < PR * PC; pp += blockDim.x) {
+    const int r = pp / PC, col = pp - r * PC;
+    const int f = f0 - back - 1 + r, w = col - 1;
+    float acc[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) acc[k] = 0.f;
+    if (f >= 0 && f < F && w >= 0 && w < W) {
+      const vec* px = (const vec*)(src + ((size_t)f * W + w) * C);
+      for (int q = 0; q < C / VE; ++q) {
+        const vec v = px[q];
+#pragma unroll
+        for (int j = 0; j < VE; ++j) {
+          const int c = q * VE + j;
+          const float sv = silu(to_f32<T>(v[j]) * gs[c] + gs[C + c]);
+#pragma unroll
+          for (int k = 0; k < 9; ++k) acc[k] += wg[c * 9 + k] * sv;   // uniform -> scalar loads
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) P[(k * PR + r) * PC + col] = acc[k];
   }
   __syncthreads();
   for (int p = tid; p < YR * W; p += blockDim.x) {
-    const int r = p / W, w = p - r * W;
+    const int r = p / W, w = p - r * W;        // y row r <-> P rows r .. r+2, cols w .. w+2
     float s = 0.f;
-    for (int tap = 0; tap < 9; ++tap) {
-      const int dy = tap / 3, dx = tap - dy * 3;
-      const float* ip = in + ((r + dy) * IC + (w + dx)) * CL;
-      const float* wp = wl + tap * C;
-      for (int c = 0; c < C; c += 4) {
-        const f32x4 v = *(const f32x4*)(ip + c);
-        s += wp[c] * v[0] + wp[c + 1] * v[1] + wp[c + 2] * v[2] + wp[c + 3] * v[3];
-      }
-    }
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx) s += P[((dy * 3 + dx) * PR + r + dy) * PC + w + dx];
     y[p] = s + a.bias;
   }
   __syncthreads();
@@ -604,27 +310,35 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   const int t = a.t_dev ? *a.t_dev : 0;
   float* xrow = a.x + (size_t)b * a.N;
   const float* crow = a.cond ? a.cond + (size_t)b * a.N : nullptr;
-  for (int n = n_begin + tid; n < n_end; n += blockDim.x) {
-    // overlapAdd (UNetModified2.py:37-39): frames in ascending order
-    int flo = (n - W + S) / S;  // ceil((n - W + 1) / S) for n >= W-1
-    if (n - W + 1 <= 0) flo = 0;
-    const int fhi = min(F - 1, n / S);
-    float e = 0.f;
-    for (int f = flo; f <= fhi; ++f) e += y[(f - (f0 - back)) * W + (n - f * S)];
-    if (a.mode < 0) {
-      a.eps_out[(size_t)b * a.N + n] = e;
-    } else {
-      const uint64_t ge = (uint64_t)((a.row_offset + b) * (int64_t)a.N + n);
-      const float z = t > 1 ? philox_normal1(a.seed, (uint32_t)t, ge) : 0.f;
-      xrow[n] = transition_one(a.mode, a.co, t, xrow[n], e, crow ? crow[n] : 0.f, z);
+  const int64_t ebase = (a.row_offset + b) * (int64_t)a.N;
+  for (int n4 = n_begin + 4 * tid; n4 < n_end; n4 += 4 * blockDim.x) {
+    const uint64_t e0 = (uint64_t)(ebase + n4);
+    f32x4 z = {0.f, 0.f, 0.f, 0.f};
+    const bool aligned = (e0 & 3) == 0;
+    if (a.mode >= 0 && t > 1 && aligned) z = philox_normal4(a.seed, (uint32_t)t, e0 >> 2);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n4 + j;
+      if (n >= n_end) break;
+      int flo = (n - W + S) / S;
+      if (n - W + 1 <= 0) flo = 0;
+      const int fhi = min(F - 1, n / S);
+      float e = 0.f;
+      for (int f = flo; f <= fhi; ++f) e += y[(f - (f0 - back)) * W + (n - f * S)];
+      if (a.mode < 0) {
+        a.eps_out[(size_t)b * a.N + n] = e;
+      } else {
+        const float zz = (t > 1) ? (aligned ? z[j] : philox_normal1(a.seed, (uint32_t)t, e0 + j)) : 0.f;
+        xrow[n] = transition_one(a.mode, a.co, t, xrow[n], e, crow ? crow[n] : 0.f, zz);
+      }
     }
   }
 }
 
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
   const int back = a.W / a.S - 1, YR = a.FT + back;
-  const size_t lds = ((size_t)(YR + 2) * (a.W + 2) * (a.C + 4) + 9 * a.C + YR * a.W + 2 * a.C) * 4;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  const size_t lds = ((size_t)9 * (YR + 2) * (a.W + 2) + (size_t)YR * a.W + 9 * a.C + 2 * a.C) * 4;
+  if (lds > 160 * 1024 || a.F % a.FT) return hipErrorInvalidValue;
   dim3 grid(a.F / a.FT, B);
   if (dtype == DT_F32) hipLaunchKernelGGL(final_kernel<float>, grid, dim3(256), lds, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(final_kernel<bf16_t>, grid, dim3(256), lds, s, a);

@@ -200,6 +200,7 @@ struct Op {
   int cls;  // 0 conv_in, 1 gn, 2 conv3x3, 3 final, 4 other
   double bytes, flops;
   std::function<hipError_t(hipStream_t)> run;
+  std::string name = "";
 };
 struct ProfAcc { double ms = 0; int64_t n = 0; double bytes = 0, flops = 0; };
 
@@ -243,6 +244,7 @@ struct sddm_ctx {
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> ev_used;  // (op cls, pool index of start event)
+  std::vector<int> ev_op;                     // op index of each timed launch
   std::vector<double> ev_bytes, ev_flops;
   std::map<int, ProfAcc> prof_acc;
 
@@ -380,24 +382,73 @@ static int upload_tables(sddm_ctx* c) {
 // ---------------------------------------------------------------------------------------------
 // plan: the launch sequence of one UNetModified2 step for batch B
 // ---------------------------------------------------------------------------------------------
-static int choose_conv_cfg(int dt, ConvArgs& a, ConvCfg& cfg, bool s2) {
+// Tile-kernel configuration: waves split K (kw) when the M x N grid alone cannot fill the chip.
+static int choose_conv_cfg(int dt, int B, ConvArgs& a, ConvCfg& cfg, bool s2) {
   const int pix = a.Ho * a.Wo;
-  const int nb_pref = (a.Cout % 64 == 0) ? 64 : 32;
-  const int mb_pref = pix >= 2048 ? 128 : 64;
-  const int nbs[2] = {nb_pref, 32};
-  const int mbs[2] = {mb_pref, 64};
-  for (int ni = 0; ni < 2; ++ni)
-    for (int mi = 0; mi < 2; ++mi) {
-      cfg.stride2 = s2 ? 1 : 0;
-      cfg.nblk = nbs[ni];
-      cfg.mblk = mbs[mi];
-      a.TW = std::min(a.Wo, cfg.mblk);
-      a.TR = std::min(cfg.mblk / a.TW, a.Ho);
-      a.tiles_x = a.Wo / a.TW;
-      a.n_tiles = a.tiles_x * (a.Ho / a.TR);
-      if (conv3x3_lds_bytes(dt, cfg, a) <= 160 * 1024) return 0;
+  const int nz = (a.Cout + 31) / 32;
+  const int nall = (a.CA + a.CB) / 32 + (a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0);
+  struct Cand { int kw, fp; };
+  std::vector<Cand> cands;
+  const int tiles128 = std::max(1, pix / 128);
+  if (tiles128 * B * nz >= 512 || nall < 2) { cands = {{1, 2}, {1, 1}, {2, 2}}; }
+  else if (nall < 4) { cands = {{2, 4}, {2, 2}, {1, 2}, {1, 1}}; }
+  else { cands = {{4, 8}, {4, 4}, {4, 2}, {2, 4}, {2, 2}, {1, 2}, {1, 1}}; }
+  for (const Cand& cd : cands) {
+    const int mblk = (4 / cd.kw) * cd.fp * 16;
+    if (cd.kw == 4 && mblk > 32 && pix < mblk / 2 * 1) {}  // keep: small images use the smaller tiles below
+    cfg.stride2 = s2 ? 1 : 0;
+    cfg.kw = cd.kw; cfg.fp = cd.fp; cfg.nblk = 32;
+    a.TW = std::min(a.Wo, mblk);
+    a.TR = std::min(mblk / a.TW, a.Ho);
+    if (a.TW * a.TR < mblk && cd.fp > 1 && pix < mblk) continue;   // image smaller than the tile: shrink
+    a.tiles_x = a.Wo / a.TW;
+    a.n_tiles = a.tiles_x * (a.Ho / a.TR);
+    if (conv3x3_lds_bytes(dt, cfg, a) <= 160 * 1024) return 0;
+  }
+  // last resort: smallest tile that fits
+  cfg.kw = 1; cfg.fp = 1; cfg.nblk = 32; cfg.stride2 = s2 ? 1 : 0;
+  a.TW = std::min(a.Wo, 64); a.TR = std::min(64 / a.TW, a.Ho);
+  a.tiles_x = a.Wo / a.TW; a.n_tiles = a.tiles_x * (a.Ho / a.TR);
+  return conv3x3_lds_bytes(dt, cfg, a) <= 160 * 1024 ? 0 : 1;
+}
+
+struct ConvChoice {
+  int strip = 0;      // 1: row-streaming kernel (conv_strip.hip), 0: tile kernel
+  ConvCfg cfg{};      // tile kernel configuration
+  int nblk = 32, SR = 0;
+  int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
+};
+
+static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
+                        ConvChoice& ch) {
+  ConvArgs a{};
+  a.CA = Cin; a.CB = 0; a.RCA = RC; a.RCB = 0; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
+  a.upsample = up ? 1 : 0;
+  a.Hi = up ? Ho / 2 : (s2 ? Ho * 2 : Ho); a.Wi = up ? Wo / 2 : (s2 ? Wo * 2 : Wo);
+  const int TRs = Wo > 0 ? 128 / Wo : 0;
+  if (!s2 && (Wo == 128 || Wo == 64) && Ho % TRs == 0) {
+    const int nbs[2] = {(Cout % 64 == 0) ? 64 : 32, 32};
+    for (int ni = 0; ni < 2; ++ni) {
+      const int nb = nbs[ni];
+      if (conv_strip_lds_bytes(dt, nb, a) > 160 * 1024) continue;
+      const int nz = (Cout + nb - 1) / nb;
+      int SR = 0;
+      for (int m = 32; m >= 2; m /= 2) {   // longest strip that still gives >= 256 blocks
+        const int sr = TRs * m;
+        if (Ho % sr) continue;
+        SR = sr;
+        if ((Ho / sr) * B * nz >= 256) break;
+      }
+      if (SR == 0) break;
+      ch.strip = 1; ch.nblk = nb; ch.SR = SR;
+      ch.TR = SR; ch.TW = Wo; ch.tiles_x = 1; ch.n_tiles = Ho / SR;
+      return true;
     }
-  return 1;
+  }
+  ch.strip = 0;
+  if (choose_conv_cfg(dt, B, a, ch.cfg, s2)) return false;
+  ch.TR = a.TR; ch.TW = a.TW; ch.tiles_x = a.tiles_x; ch.n_tiles = a.n_tiles;
+  return true;
 }
 
 static int build_plan(sddm_ctx* c, int B) {
@@ -422,10 +473,10 @@ static int build_plan(sddm_ctx* c, int B) {
     tres.push_back(t);
     return (int)tres.size() - 1;
   };
-  struct GNRes { size_t sc, sh; };
+  struct GNRes { int a, b; std::string w; };   // GroupNorm sources (finalized in the consumer)
   std::vector<GNRes> gres;
-  auto new_gn = [&](int C) -> int {
-    gres.push_back({A.reserve(sizeof(float) * B * C), A.reserve(sizeof(float) * B * C)});
+  auto new_gn = [&](int xa, int xb, const std::string& w) -> int {
+    gres.push_back({xa, xb, w});
     return (int)gres.size() - 1;
   };
   c->off_temb_fwd = A.reserve(sizeof(float) * (size_t)B * std::max(c->SC, 1));
@@ -439,14 +490,11 @@ static int build_plan(sddm_ctx* c, int B) {
     int srcA = -1, srcB = -1, gn = -1, out = -1;
     int s2 = 0, up = 0, res_mode = 0, rawA = -1, rawB = -1, cout = 0;
     bool temb = false;
+    ConvChoice ch;
   };
   std::vector<Step> prog;
-  auto geom = [&](int Ho, int Wo, int cout, bool s2, int& tiles, int& n_tile) -> bool {
-    ConvArgs a{}; a.Ho = Ho; a.Wo = Wo; a.Cout = cout; a.res_mode = 2;  // worst-case LDS
-    ConvCfg cfg;
-    if (choose_conv_cfg(dt, a, cfg, s2)) return false;
-    tiles = a.n_tiles; n_tile = a.TR * a.TW;
-    return true;
+  auto pick = [&](int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up, ConvChoice& ch) {
+    return choose_conv(dt, B, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch);
   };
   const int TRin = 2;
   if (F % TRin) FAIL(SDDM_ERR_SHAPE, "n_frames %d not even", F);
@@ -455,18 +503,17 @@ static int build_plan(sddm_ctx* c, int B) {
 
   auto res_block = [&](const std::string& n, int xa, int xb, int cin, int cout) -> int {
     const int H = tres[xa].H, Wd = tres[xa].W;
-    int tiles, nt;
-    if (!geom(H, Wd, cout, false, tiles, nt)) return -1;
-    const int g1 = new_gn(cin);
-    { Step st; st.type = ST_GN; st.w = n + ".block1"; st.srcA = xa; st.srcB = xb; st.gn = g1; prog.push_back(st); }
-    const int h = new_tensor(cout, H, Wd, tiles, nt);
+    ConvChoice c1, c2;
+    if (!pick(cin, 0, 0, H, Wd, cout, false, false, c1)) return -1;
+    if (!pick(cout, cin, cin != cout ? 2 : 1, H, Wd, cout, false, false, c2)) return -1;
+    const int g1 = new_gn(xa, xb, n + ".block1");
+    const int h = new_tensor(cout, H, Wd, c1.n_tiles, c1.TR * c1.TW);
     { Step st; st.type = ST_CONV; st.w = n + ".block1"; st.rb = n; st.srcA = xa; st.srcB = xb; st.gn = g1;
-      st.out = h; st.cout = cout; st.temb = true; prog.push_back(st); }
-    const int g2 = new_gn(cout);
-    { Step st; st.type = ST_GN; st.w = n + ".block2"; st.srcA = h; st.gn = g2; prog.push_back(st); }
-    const int o = new_tensor(cout, H, Wd, tiles, nt);
+      st.out = h; st.cout = cout; st.temb = true; st.ch = c1; prog.push_back(st); }
+    const int g2 = new_gn(h, -1, n + ".block2");
+    const int o = new_tensor(cout, H, Wd, c2.n_tiles, c2.TR * c2.TW);
     { Step st; st.type = ST_CONV; st.w = n + ".block2"; st.rb = n; st.srcA = h; st.gn = g2; st.out = o;
-      st.cout = cout; st.res_mode = cin != cout ? 2 : 1; st.rawA = xa; st.rawB = xb; prog.push_back(st); }
+      st.cout = cout; st.res_mode = cin != cout ? 2 : 1; st.rawA = xa; st.rawB = xb; st.ch = c2; prog.push_back(st); }
     return o;
   };
   std::vector<LayerDesc> downs, mid, ups;
@@ -480,10 +527,10 @@ static int build_plan(sddm_ctx* c, int B) {
     } else {
       if (tres[cur].H % 2 || tres[cur].W % 2) FAIL(SDDM_ERR_SHAPE, "odd size before %s", L.name.c_str());
       const int H = tres[cur].H / 2, Wd = tres[cur].W / 2;
-      int tiles, nt;
-      if (!geom(H, Wd, L.cout, true, tiles, nt)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
-      const int o = new_tensor(L.cout, H, Wd, tiles, nt);
-      Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.s2 = 1; st.cout = L.cout;
+      ConvChoice ch;
+      if (!pick(tres[cur].C, 0, 0, H, Wd, L.cout, true, false, ch)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+      const int o = new_tensor(L.cout, H, Wd, ch.n_tiles, ch.TR * ch.TW);
+      Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.s2 = 1; st.cout = L.cout; st.ch = ch;
       prog.push_back(st);
       cur = o;
     }
@@ -504,16 +551,15 @@ static int build_plan(sddm_ctx* c, int B) {
       if (cur < 0) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
     } else {
       const int H = tres[cur].H * 2, Wd = tres[cur].W * 2;
-      int tiles, nt;
-      if (!geom(H, Wd, L.cout, false, tiles, nt)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
-      const int o = new_tensor(L.cout, H, Wd, tiles, nt);
-      Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.up = 1; st.cout = L.cout;
+      ConvChoice ch;
+      if (!pick(tres[cur].C, 0, 0, H, Wd, L.cout, false, true, ch)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+      const int o = new_tensor(L.cout, H, Wd, ch.n_tiles, ch.TR * ch.TW);
+      Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.up = 1; st.cout = L.cout; st.ch = ch;
       prog.push_back(st);
       cur = o;
     }
   }
-  const int gf = new_gn(tres[cur].C);
-  { Step st; st.type = ST_GN; st.w = "final_conv"; st.srcA = cur; st.gn = gf; prog.push_back(st); }
+  const int gf = new_gn(cur, -1, "final_conv");
   { Step st; st.type = ST_FINAL; st.srcA = cur; st.gn = gf; prog.push_back(st); }
   SDDM_HIP_CHECK(A.commit());
 
@@ -542,26 +588,23 @@ static int build_plan(sddm_ctx* c, int B) {
                           ConvInArgs x = a;
                           x.cond = ctx->rs.cond; x.x = ctx->rs.x; x.t_dev = ctx->rs.t_dev;
                           return launch_conv_in(dt, x, B, s);
-                        }});
-    } else if (st.type == ST_GN) {
-      GNArgs g{};
-      const Tensor ta = TT(st.srcA), tb = TT(st.srcB);
-      g.a = {ta.stats, ta.C, ta.tiles, ta.n_tile};
-      g.b = {tb.stats, tb.C, tb.tiles, tb.n_tile};
-      g.gamma = WF(st.w + ".gamma"); g.beta = WF(st.w + ".beta");
-      g.G = u.groups; g.eps = 1e-5f; g.B = B;
-      if ((ta.C + tb.C) % u.groups)
-        FAIL(SDDM_ERR_SHAPE, "GroupNorm(%d, %d): channels not divisible by groups", u.groups, ta.C + tb.C);
-      g.scale = A.at<float>(gres[st.gn].sc); g.shift = A.at<float>(gres[st.gn].sh);
-      const double bytes = (double)B * (ta.tiles * ta.C + tb.tiles * tb.C) * 8;
-      c->ops.push_back({1, bytes, 0.0, [g](hipStream_t s) { return launch_gn_finalize(g, s); }});
+                        }, "downs.0"});
     } else if (st.type == ST_CONV) {
       ConvArgs a{};
       const Tensor sa = TT(st.srcA), sb = TT(st.srcB), o = TT(st.out);
       a.srcA = sa.p; a.srcB = sb.p; a.CA = sa.C; a.CB = sb.C;
       a.Hi = sa.H; a.Wi = sa.W; a.Ho = o.H; a.Wo = o.W; a.upsample = st.up;
       a.Cout = st.cout; a.out = o.p; a.stats = o.stats;
-      if (st.gn >= 0) { a.gn_scale = A.at<float>(gres[st.gn].sc); a.gn_shift = A.at<float>(gres[st.gn].sh); }
+      if (st.gn >= 0) {
+        const GNRes& gr = gres[st.gn];
+        const Tensor ga = TT(gr.a), gb = TT(gr.b);
+        a.gstA = ga.stats; a.gtilesA = ga.tiles; a.gntileA = ga.n_tile;
+        a.gstB = gb.stats; a.gtilesB = gb.tiles; a.gntileB = gb.n_tile;
+        a.gamma = WF(gr.w + ".gamma"); a.beta = WF(gr.w + ".beta"); a.groups = u.groups; a.eps = 1e-5f;
+        const int Ct = ga.C + gb.C;
+        if (Ct % u.groups || (gb.C && ga.C % (Ct / u.groups)) || 256 % u.groups)
+          FAIL(SDDM_ERR_SHAPE, "GroupNorm(%d, %d) at %s: unsupported grouping", u.groups, Ct, gr.w.c_str());
+      }
       a.wgt = WV(st.w + ".w"); a.bias = WF(st.w + ".b");
       a.res_mode = st.res_mode;
       const int Cin = a.CA + a.CB;
@@ -579,18 +622,14 @@ static int build_plan(sddm_ctx* c, int B) {
         bytes += (double)B * a.Ho * a.Wo * (ra.C + rb.C) * es + (double)a.Cout * (ra.C + rb.C) * es;
         flops += 2.0 * B * a.Ho * a.Wo * a.Cout * (double)(ra.C + rb.C);
       }
-      ConvCfg cfg;
-      {  // same (worst-case LDS) choice as pass 1, so the stats tiling matches the tensor
-        ConvArgs probe = a;
-        probe.res_mode = 2;
-        if (choose_conv_cfg(dt, probe, cfg, st.s2)) FAIL(SDDM_ERR_SHAPE, "no conv tile fits LDS for %s", st.w.c_str());
-        a.TR = probe.TR; a.TW = probe.TW; a.tiles_x = probe.tiles_x; a.n_tiles = probe.n_tiles;
-        if (a.n_tiles != o.tiles || a.TR * a.TW != o.n_tile) FAIL(SDDM_ERR_STATE, "tile mismatch for %s", st.w.c_str());
-      }
+      const ConvChoice ch = st.ch;
+      const ConvCfg cfg = ch.cfg;
+      a.TR = ch.TR; a.TW = ch.TW; a.tiles_x = ch.tiles_x; a.n_tiles = ch.n_tiles;
+      if (a.n_tiles != o.tiles || a.TR * a.TW != o.n_tile) FAIL(SDDM_ERR_STATE, "tile mismatch for %s", st.w.c_str());
       if (Cin % 32 || a.Cout % 32) FAIL(SDDM_ERR_SHAPE, "%s: channels must be multiples of 32", st.w.c_str());
       const bool temb = st.temb;
       const int toff = temb ? c->temb_off.at(st.rb) : 0;
-      c->ops.push_back({2, bytes, flops, [ctx, a, cfg, dt, B, temb, toff](hipStream_t s) {
+      c->ops.push_back({2, bytes, flops, [ctx, a, cfg, ch, dt, B, temb, toff](hipStream_t s) {
                           ConvArgs x = a;
                           if (temb) {
                             x.temb = ctx->rs.temb + toff;
@@ -598,16 +637,23 @@ static int build_plan(sddm_ctx* c, int B) {
                             x.temb_per_b = ctx->rs.temb_per_b;
                             x.t_dev = ctx->rs.t_dev;
                           }
+                          if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.SR, x, B, s);
                           return launch_conv3x3(dt, cfg, x, B, s);
-                        }});
+                        }, st.w + (ch.strip ? "[strip]" : "")});
     } else {
       FinalArgs f{};
       const Tensor src = TT(st.srcA);
       f.src = src.p; f.C = src.C;
-      f.gn_scale = A.at<float>(gres[st.gn].sc); f.gn_shift = A.at<float>(gres[st.gn].sh);
+      {
+        const GNRes& gr = gres[st.gn];
+        const Tensor ga = TT(gr.a);
+        f.gst = ga.stats; f.gtiles = ga.tiles; f.gntile = ga.n_tile;
+        f.gamma = WF("final_conv.gamma"); f.beta = WF("final_conv.beta"); f.groups = u.groups; f.eps = 1e-5f;
+        if (ga.C % u.groups || 256 % u.groups) FAIL(SDDM_ERR_SHAPE, "final GroupNorm grouping");
+      }
       f.w = WF("final_conv.w");
       f.bias = c->params.at("final_conv.block.3.bias").data[0];
-      f.N = N; f.F = F; f.W = W; f.S = S; f.FT = 2;
+      f.N = N; f.F = F; f.W = W; f.S = S; f.FT = F % 8 == 0 ? 8 : 2;
       if (F % f.FT || W % S) FAIL(SDDM_ERR_SHAPE, "final tile: frames %d, segment %d/%d", F, W, S);
       f.co = c->coef();
       const double bytes = (double)B * F * W * src.C * es + (double)B * N * 4 * 3;
@@ -618,7 +664,7 @@ static int build_plan(sddm_ctx* c, int B) {
                           x.x = ctx->rs.x; x.cond = ctx->rs.cond; x.t_dev = ctx->rs.t_dev;
                           x.seed = ctx->rs.seed; x.row_offset = ctx->rs.row_offset;
                           return launch_final(dt, x, B, s);
-                        }});
+                        }, "final_conv"});
     }
   }
   c->plan_B = B;
@@ -658,6 +704,7 @@ static int run_ops(sddm_ctx* c, hipStream_t s) {
     if (timed) {
       SDDM_HIP_CHECK(hipEventRecord(c->ev_pool[e0 + 1], s));
       c->ev_used.push_back({op.cls, e0});
+      c->ev_op.push_back((int)(&op - c->ops.data()));
       c->ev_bytes.push_back(op.bytes);
       c->ev_flops.push_back(op.flops);
     }
@@ -988,7 +1035,7 @@ int sddm_profile_enable(sddm_ctx* c, int enable) {
   if (!c) FAIL(SDDM_ERR_INVALID_ARG, "NULL ctx");
   SDDM_HIP_CHECK(hipSetDevice(c->device));
   c->prof = enable != 0;
-  c->ev_used.clear(); c->ev_bytes.clear(); c->ev_flops.clear(); c->prof_acc.clear();
+  c->ev_used.clear(); c->ev_bytes.clear(); c->ev_flops.clear(); c->prof_acc.clear(); c->ev_op.clear();
   if (c->prof && c->ev_pool.empty()) {
     c->ev_pool.resize(20000);
     for (auto& e : c->ev_pool) SDDM_HIP_CHECK(hipEventCreate(&e));
@@ -1017,6 +1064,32 @@ int sddm_profile_read(sddm_ctx* c, const char* kernel_class, double* avg_ms, int
   if (launches) *launches = n;
   if (bytes_per_launch) *bytes_per_launch = n ? bytes / n : 0.0;
   if (flops_per_launch) *flops_per_launch = n ? flops / n : 0.0;
+  return SDDM_OK;
+}
+
+int sddm_profile_ops(sddm_ctx* c, char* buf, int64_t buflen) {
+  if (!c || !buf || buflen < 3) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
+  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  std::vector<double> ms(c->ops.size(), 0.0);
+  std::vector<int64_t> n(c->ops.size(), 0);
+  for (size_t i = 0; i < c->ev_used.size(); ++i) {
+    const int e0 = c->ev_used[i].second, op = c->ev_op[i];
+    SDDM_HIP_CHECK(hipEventSynchronize(c->ev_pool[e0 + 1]));
+    float m = 0;
+    SDDM_HIP_CHECK(hipEventElapsedTime(&m, c->ev_pool[e0], c->ev_pool[e0 + 1]));
+    if (op >= 0 && op < (int)ms.size()) { ms[op] += m; ++n[op]; }
+  }
+  std::string js = "[";
+  char tmp[512];
+  for (size_t i = 0; i < c->ops.size(); ++i) {
+    snprintf(tmp, sizeof(tmp), "%s{\"name\": \"%s\", \"cls\": %d, \"launches\": %lld, \"avg_ms\": %.6f, \"bytes\": %.0f, \"flops\": %.0f}",
+             i ? ", " : "", c->ops[i].name.c_str(), c->ops[i].cls, (long long)n[i], n[i] ? ms[i] / n[i] : 0.0,
+             c->ops[i].bytes, c->ops[i].flops);
+    js += tmp;
+  }
+  js += "]";
+  if ((int64_t)js.size() + 1 > buflen) FAIL(SDDM_ERR_INVALID_ARG, "buffer too small (%zu)", js.size() + 1);
+  std::memcpy(buf, js.c_str(), js.size() + 1);
   return SDDM_OK;
 }
 

@@ -26,7 +26,7 @@ EXPORTS = ("sddm_abi_version", "sddm_last_error", "sddm_create", "sddm_destroy",
            "sddm_load_param", "sddm_missing_params", "sddm_sample", "sddm_sample_continuous",
            "sddm_network_forward",
            "sddm_transition", "sddm_initial_state", "sddm_schedule", "sddm_profile_enable",
-           "sddm_profile_read")
+           "sddm_profile_read", "sddm_profile_ops")
 
 _lib = None
 
@@ -58,6 +58,7 @@ def lib():
         L.sddm_profile_read.argtypes = [vp, ctypes.c_char_p, ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(i64), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)]
+        L.sddm_profile_ops.argtypes = [vp, ctypes.c_char_p, i64]
         for name in EXPORTS:
             if name not in ("sddm_last_error", "sddm_destroy", "sddm_abi_version"):
                 getattr(L, name).restype = c_int
@@ -179,3 +180,8 @@ class Context:
         check(lib().sddm_profile_read(self._h, kernel_class.encode(), ctypes.byref(ms), ctypes.byref(n),
                                       ctypes.byref(b), ctypes.byref(f)))
         return dict(avg_ms=ms.value, launches=n.value, bytes_per_launch=b.value, flops_per_launch=f.value)
+
+    def profile_ops(self):
+        buf = ctypes.create_string_buffer(1 << 20)
+        check(lib().sddm_profile_ops(self._h, buf, len(buf)))
+        return json.loads(buf.value.decode())

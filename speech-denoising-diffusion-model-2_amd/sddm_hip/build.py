@@ -18,7 +18,7 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
 BUILD = os.path.join(HERE, "_build")
 LIB = os.path.join(HERE, "libsddm_hip.so")
-SOURCES = ["kernels.hip", "sddm_runtime.cpp", "schedule.cpp"]
+SOURCES = ["kernels.hip", "conv_strip.hip", "conv_tile.hip", "sddm_runtime.cpp", "schedule.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SDDM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
@@ -51,7 +51,7 @@ def build(verbose=False):
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(_compile, SOURCES))
     if _stale(LIB, objs):
-        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-o", LIB] + objs
+        cmd = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-Wl,--no-undefined", "-o", LIB] + objs
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
