@@ -173,3 +173,27 @@ __device__ __forceinline__ void tile_channel_stats(const float* tile, int ld, in
 }
 
 }  // namespace sddm
+
+namespace sddm {
+
+__device__ __forceinline__ float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+
+template <typename T>
+__device__ __forceinline__ f32x4 transform_fast(f32x4 raw, const float* sc, const float* sh) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(VE)));
+  vec v = __builtin_bit_cast(vec, raw);
+#pragma unroll
+  for (int j = 0; j < VE; ++j) v[j] = from_f32<T>(silu_fast(to_f32<T>(v[j]) * sc[j] + sh[j]));
+  return __builtin_bit_cast(f32x4, v);
+}
+
+// an MFMA operand fragment whose 16-byte units sit in consecutive planes `stride` bytes apart
+template <typename T> __device__ __forceinline__ Frag<T> load_planes(const char* p, int stride);
+template <> __device__ __forceinline__ Frag<bf16_t> load_planes<bf16_t>(const char* p, int) { return {*(const bf16x8*)p}; }
+template <> __device__ __forceinline__ Frag<f16_t> load_planes<f16_t>(const char* p, int) { return {*(const f16x8*)p}; }
+template <> __device__ __forceinline__ Frag<float> load_planes<float>(const char* p, int stride) {
+  return {*(const f32x4*)p, *(const f32x4*)(p + stride)};
+}
+
+}  // namespace sddm

@@ -3,13 +3,19 @@
 //
 // One block owns image b, output channels [n0, n0 + 16*FC) and a strip of SR output rows.  It
 // keeps in LDS
-//   * the whole weight slab of its channel tile (loaded once per strip, not once per tile), and
+//   * the weight slab of its channel tile (loaded once per strip, not once per tile), and
 //   * a ring of R = 2*TR + 2 transformed input rows (GroupNorm + SiLU applied once per element,
 //     zero halo columns, nearest-2x upsample / channel concat resolved while loading),
 // and walks the strip TR = 128 / W output rows at a time (128 pixels = 4 waves x 2 MFMA column
 // fragments).  While the MFMAs of iteration i run on rows [y-1, y+TR] of the ring, each thread
 // already holds in registers the raw input of rows [y+TR+1, y+2TR] (issued before the MFMAs) and
 // writes them transformed into the free ring slots afterwards: one barrier per iteration.
+//
+// LDS images are plane-major (a plane = one 16-byte channel unit of every pixel / output channel,
+// plane stride = 0 mod 256 B): the 16 lanes of an MFMA operand read 16 consecutive 16-byte slots
+// and the ds_read_b128 lane groups never collide; staging writes go 8 consecutive pixels per
+// 8-lane group (conflict free) while the 64 lanes of a wave read 64/UPP whole pixels (coalesced).
+// Geometry (W, Cin) is compile-time so no integer division runs per element.
 // The epilogue adds bias, the noise-embedding projection and the residual (identity, or the
 // ResnetBlock 1x1 res_conv as extra MFMAs on raw input fragments loaded straight to registers),
 // stores 4 channels per lane, and accumulates GroupNorm statistics of the stored values in
@@ -19,65 +25,64 @@
 
 namespace sddm {
 
-template <typename T, int FC, int MAXU>
-__global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int TR, int SR) {
-  constexpr int FP = 2;
+template <typename T, int FC, int W, int CIN>
+__global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
   constexpr int ES = (int)sizeof(T);
-  constexpr int NBLK = 16 * FC;
-  constexpr int LG = 8 * ES;        // bytes of a lane group's 8 channels
+  constexpr int NBLK = 16 * FC, FP = 2;
+  constexpr int TR = 128 / W, R = 2 * TR + 2;
+  constexpr int UPP = CIN * ES / 16;              // 16-byte channel units (planes) per pixel
+  constexpr int UPL = ES / 2;                     // units per lane group (8 channels)
+  constexpr int VE = 16 / ES;
+  constexpr int PL = ((W + 2) * 16 + 255) / 256 * 256;
+  constexpr int SLOT = UPP * PL;
+  constexpr int NCK = CIN / 32;
+  constexpr int WPL = NBLK * 16;                  // weight plane stride
+  constexpr int WPLANES = NCK * 9 * 4 * UPL;
+  constexpr int PB = 64 / UPP;                    // pixels per 64-unit staging group
+  constexpr int NU = TR * W * UPP;                // units of TR rows
+  constexpr int UPT = NU / 256;                   // prefetch units per thread
+  static_assert(UPP >= 1 && UPP <= 64 && (64 % UPP) == 0, "channel units must divide a wave");
+  static_assert(NU % 256 == 0, "prefetch must split evenly");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int strip = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NBLK;
-  const int W = a.Wo, H = a.Ho;
-  const int Cin = a.CA + a.CB, nck = Cin / 32;
-  const int R = 2 * TR + 2;
-  const int PIXB = Cin * ES + 16;
-  const int SLOT = (W + 2) * PIXB;
-  const int WROW = nck * 9 * 32 * ES + 16;
+  const int H = a.Ho;
   const int RC = a.RCA + a.RCB;
-  const int RROW = RC * ES + 16;
   const bool gn = a.gamma != nullptr;
   const bool res2 = a.res_mode == 2;
-  const int UPP = Cin * ES / 16;    // 16-byte units per pixel
-  const int VE = 16 / ES;
 
-  char* ring = smem;
-  char* wl = ring + R * SLOT;
-  char* rw = wl + NBLK * WROW;
-  float* gsc = (float*)(rw + (res2 ? NBLK * RROW : 0));
-  float* red = gsc + 2 * Cin;       // [4 waves][NBLK][3]
+  char* ring = smem;                              // [R][UPP planes][PL]
+  char* wl = ring + R * SLOT;                     // [WPLANES][NBLK][16 B]
+  char* rw = wl + WPLANES * WPL;                  // [RC*ES/16 planes][NBLK][16 B]
+  const int RPLANES = res2 ? RC * ES / 16 : 0;
+  float* gsc = (float*)(rw + RPLANES * WPL);      // [2][CIN]
+  float* red = gsc + 2 * CIN;                     // [4 waves][NBLK][3]
 
   const int y0 = strip * SR;
   // ---------------- prologue ----------------
   if (gn) {
     const GNFuse f{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-    gn_fused_prologue(f, b, a.CA, a.CB, gsc, gsc + Cin);
+    gn_fused_prologue(f, b, a.CA, a.CB, gsc, gsc + CIN);
   }
-  {
-    const int upr = (WROW - 16) / 16;
-    for (int u = tid; u < NBLK * upr; u += 256) {
-      const int row = u / upr, q = u - row * upr;
-      *(f32x4*)(wl + row * WROW + q * 16) =
-          *(const f32x4*)((const char*)a.wgt + (size_t)(n0 + row) * (WROW - 16) + q * 16);
-    }
-    if (res2) {
-      const int rpr = RC * ES / 16;
-      for (int u = tid; u < NBLK * rpr; u += 256) {
-        const int row = u / rpr, q = u - row * rpr;
-        *(f32x4*)(rw + row * RROW + q * 16) =
-            *(const f32x4*)((const char*)a.res_wgt + ((size_t)(n0 + row) * RC) * ES + q * 16);
-      }
-    }
-    // zero halo columns of every slot
-    for (int u = tid; u < R * 2 * UPP; u += 256) {
-      const int s = u / (2 * UPP), rem = u - s * 2 * UPP, side = rem / UPP, q = rem - side * UPP;
-      *(f32x4*)(ring + s * SLOT + (side ? (W + 1) : 0) * PIXB + q * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int u = tid; u < NBLK * WPLANES; u += 256) {       // co fastest: conflict-free LDS writes
+    const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
+    const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
+    *(f32x4*)(wl + pl * WPL + co * 16) =
+        *(const f32x4*)((const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16);
+  }
+  if (res2) {
+    for (int u = tid; u < NBLK * RPLANES; u += 256) {
+      const int co = u % NBLK, pl = u / NBLK;
+      *(f32x4*)(rw + pl * WPL + co * 16) = *(const f32x4*)((const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16);
     }
   }
-  __syncthreads();
+  for (int u = tid; u < R * UPP * 2; u += 256) {          // zero halo columns
+    const int side = u & 1, pl = u >> 1;
+    *(f32x4*)(ring + pl * PL + (side ? (W + 1) : 0) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();                                         // gsc ready
 
-  // raw 16-byte unit of output-space input row ry, column x, channel unit q (zero outside the image)
   auto load_unit = [&](int ry, int x, int q) -> f32x4 {
     if (ry < 0 || ry >= H) return f32x4{0.f, 0.f, 0.f, 0.f};
     int sy = ry, sx = x;
@@ -87,31 +92,36 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int TR, int
     if (c0 < a.CA) return *(const f32x4*)((const T*)a.srcA + pix * a.CA + c0);
     return *(const f32x4*)((const T*)a.srcB + pix * a.CB + (c0 - a.CA));
   };
-  auto row_valid = [&](int ry) { return ry >= 0 && ry < H; };
+  const int base = ((y0 - 1) % R + R) % R;                 // ring slot of row y0 - 1
 
   // initial rows y0-1 .. y0+TR
-  {
-    const int n = (TR + 2) * W * UPP;
-    for (int u = tid; u < n; u += 256) {
-      const int p = u / UPP, q = u - p * UPP, r = p / W, x = p - r * W;
-      const int ry = y0 - 1 + r;
-      const f32x4 raw = load_unit(ry, x, q);
-      const f32x4 v = row_valid(ry) ? transform_vec<T>(raw, gsc + q * VE, gsc + Cin + q * VE, gn) : raw;
-      const int slot = ((ry % R) + R) % R;
-      *(f32x4*)(ring + slot * SLOT + (x + 1) * PIXB + q * 16) = v;
-    }
+  for (int u = tid; u < (TR + 2) * W * UPP; u += 256) {
+    const int grp = u >> 6, j = u & 63;
+    const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
+    const int ry = y0 - 1 + r;
+    f32x4 v = load_unit(ry, x, q);
+    if (gn && ry >= 0 && ry < H) v = transform_fast<T>(v, gsc + q * VE, gsc + CIN + q * VE);
+    *(f32x4*)(ring + ((base + r) % R) * SLOT + q * PL + (x + 1) * 16) = v;
   }
   __syncthreads();
 
-  // per-lane pixel geometry inside an iteration (128 pixels = TR rows x W)
   int prow[FP], pcol[FP];
 #pragma unroll
   for (int fp = 0; fp < FP; ++fp) {
     const int p = wave * 32 + fp * 16 + (lane & 15);
     prow[fp] = p / W;
-    pcol[fp] = p - prow[fp] * W;
+    pcol[fp] = p % W;
   }
-  // running GroupNorm statistics (shift K = first value seen)
+  // prefetch geometry of this thread's units (same every iteration)
+  int pr[UPT], px[UPT], pq[UPT];
+#pragma unroll
+  for (int k = 0; k < UPT; ++k) {
+    const int u = tid + k * 256, grp = u >> 6, j = u & 63;
+    const int pix = grp * PB + (j % PB);
+    pq[k] = j / PB;
+    pr[k] = pix / W;
+    px[k] = pix % W;
+  }
   float sK[FC][4], s1[FC][4], s2[FC][4];
 #pragma unroll
   for (int fc = 0; fc < FC; ++fc)
@@ -127,54 +137,49 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int TR, int
       const int co = n0 + fc * 16 + 4 * g + i;
       badd[fc][i] = (co < a.Cout) ? a.bias[co] + (trow ? trow[co] : 0.f) : 0.f;
     }
+  const char* abase = wl + g * UPL * WPL + (lane & 15) * 16;
+  const char* rbase = rw + g * UPL * WPL + (lane & 15) * 16;
 
   const int iters = SR / TR;
-  const int npre = TR * W * UPP;    // units of the TR rows prefetched per iteration
   for (int it = 0; it < iters; ++it) {
     const int y = y0 + it * TR;
+    const int s_it = (base + it * TR) % R;                 // slot of row y - 1
     // ---- issue the prefetch of rows y+TR+1 .. y+2TR (raw) ----
-    f32x4 pre[MAXU];
+    f32x4 pre[UPT];
     const bool do_pre = it + 1 < iters;
+    if (do_pre) {
 #pragma unroll
-    for (int k = 0; k < MAXU; ++k) {
-      const int u = tid + k * 256;
-      if (do_pre && u < npre) {
-        const int p = u / UPP, q = u - p * UPP, r = p / W, x = p - r * W;
-        pre[k] = load_unit(y + TR + 1 + r, x, q);
-      }
+      for (int k = 0; k < UPT; ++k) pre[k] = load_unit(y + TR + 1 + pr[k], px[k], pq[k]);
     }
-    // ---- MFMA over the 9 taps x Cin/32 chunks of the current rows ----
+    // ---- MFMA over the 9 taps x CIN/32 chunks of the current rows ----
     f32x4 acc[FP][FC];
 #pragma unroll
     for (int i = 0; i < FP; ++i)
 #pragma unroll
       for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    int rowoff[FP][3];
+    const char* bptr[FP][3];
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp)
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy) {
-        const int ry = y + prow[fp] + dy - 1;
-        rowoff[fp][dy] = (((ry % R) + R) % R) * SLOT + pcol[fp] * PIXB + g * LG;
-      }
-    const char* wbase = wl + (lane & 15) * WROW + g * LG;
-    for (int ck = 0; ck < nck; ++ck) {
+      for (int dy = 0; dy < 3; ++dy)
+        bptr[fp][dy] = ring + ((s_it + prow[fp] + dy) % R) * SLOT + g * UPL * PL + pcol[fp] * 16;
+#pragma unroll
+    for (int ck = 0; ck < NCK; ++ck) {
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int dy = tap / 3, dx = tap - 3 * dy;
         Frag<T> bf[FP];
 #pragma unroll
-        for (int fp = 0; fp < FP; ++fp) bf[fp] = load_frag<T>(ring + rowoff[fp][dy] + dx * PIXB + ck * 32 * ES);
+        for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(bptr[fp][dy] + ck * 4 * UPL * PL + dx * 16, PL);
 #pragma unroll
         for (int fc = 0; fc < FC; ++fc) {
-          const Frag<T> af = load_frag<T>(wbase + fc * 16 * WROW + (ck * 9 + tap) * 32 * ES);
+          const Frag<T> af = load_planes<T>(abase + (ck * 9 + tap) * 4 * UPL * WPL + fc * 256, WPL);
 #pragma unroll
           for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
         }
       }
     }
     if (res2) {  // ResnetBlock.res_conv 1x1 on the raw block input, B fragments straight from global
-      const char* rbase = rw + (lane & 15) * RROW + g * LG;
       for (int ck = 0; ck < RC / 32; ++ck) {
         Frag<T> bf[FP];
 #pragma unroll
@@ -186,7 +191,7 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int TR, int
         }
 #pragma unroll
         for (int fc = 0; fc < FC; ++fc) {
-          const Frag<T> af = load_frag<T>(rbase + fc * 16 * RROW + ck * 32 * ES);
+          const Frag<T> af = load_planes<T>(rbase + ck * 4 * UPL * WPL + fc * 256, WPL);
 #pragma unroll
           for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
         }
@@ -226,14 +231,11 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int TR, int
     // ---- transform the prefetched rows into the free ring slots ----
     if (do_pre) {
 #pragma unroll
-      for (int k = 0; k < MAXU; ++k) {
-        const int u = tid + k * 256;
-        if (u < npre) {
-          const int p = u / UPP, q = u - p * UPP, r = p / W, x = p - r * W;
-          const int ry = y + TR + 1 + r;
-          const f32x4 v = row_valid(ry) ? transform_vec<T>(pre[k], gsc + q * VE, gsc + Cin + q * VE, gn) : pre[k];
-          *(f32x4*)(ring + (((ry % R) + R) % R) * SLOT + (x + 1) * PIXB + q * 16) = v;
-        }
+      for (int k = 0; k < UPT; ++k) {
+        const int ry = y + TR + 1 + pr[k];
+        f32x4 v = pre[k];
+        if (gn && ry < H) v = transform_fast<T>(v, gsc + pq[k] * VE, gsc + CIN + pq[k] * VE);
+        *(f32x4*)(ring + ((s_it + TR + 2 + pr[k]) % R) * SLOT + pq[k] * PL + (px[k] + 1) * 16) = v;
       }
     }
     __syncthreads();
@@ -279,38 +281,38 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int TR, int
   }
 }
 
-template <typename T, int FC>
-static size_t strip_lds(const ConvArgs& a, int TR) {
-  constexpr int ES = (int)sizeof(T), NBLK = 16 * FC;
-  const int Cin = a.CA + a.CB;
-  const int R = 2 * TR + 2;
-  size_t n = (size_t)R * (a.Wo + 2) * (Cin * ES + 16) + (size_t)NBLK * ((Cin / 32) * 9 * 32 * ES + 16);
-  if (a.res_mode == 2) n += (size_t)NBLK * ((a.RCA + a.RCB) * ES + 16);
-  n += (size_t)2 * Cin * 4 + (size_t)4 * NBLK * 3 * 4;
+template <typename T, int FC, int W, int CIN>
+static size_t strip_lds(const ConvArgs& a) {
+  constexpr int ES = (int)sizeof(T), NBLK = 16 * FC, TR = 128 / W, R = 2 * TR + 2;
+  constexpr int UPP = CIN * ES / 16, PL = ((W + 2) * 16 + 255) / 256 * 256;
+  size_t n = (size_t)R * UPP * PL + (size_t)(CIN / 32) * 9 * 4 * (ES / 2) * NBLK * 16;
+  if (a.res_mode == 2) n += (size_t)((a.RCA + a.RCB) * ES / 16) * NBLK * 16;
+  n += (size_t)2 * CIN * 4 + (size_t)4 * NBLK * 3 * 4;
   return n;
 }
 
-template <typename T>
-static hipError_t strip_dispatch(const ConvArgs& a, int nblk, int SR, int B, hipStream_t s, size_t* lds_only) {
-  const int TR = 128 / a.Wo;
-  const size_t lds = nblk == 64 ? strip_lds<T, 4>(a, TR) : strip_lds<T, 2>(a, TR);
-  if (lds_only) { *lds_only = lds; return hipSuccess; }
-  const int Cin = a.CA + a.CB;
-  const int units = TR * a.Wo * Cin * (int)sizeof(T) / 16;
-  if (lds > 160 * 1024 || a.Wo * TR != 128 || a.Ho % SR || SR % TR || units > 16 * 256 || Cin % 32)
-    return hipErrorInvalidValue;
-  const int nz = (a.Cout + nblk - 1) / nblk;
-  dim3 grid(a.Ho / SR, B, nz);
-  const int upt = (units + 255) / 256;
-#define SDDM_STRIP(FCV, UV)                                                                        \
-  hipLaunchKernelGGL((conv_strip_kernel<T, FCV, UV>), grid, dim3(256), lds, s, a, TR, SR);
-  if (nblk == 64) {
-    if (upt <= 2) { SDDM_STRIP(4, 2) } else if (upt <= 4) { SDDM_STRIP(4, 4) } else if (upt <= 8) { SDDM_STRIP(4, 8) } else { SDDM_STRIP(4, 16) }
-  } else {
-    if (upt <= 2) { SDDM_STRIP(2, 2) } else if (upt <= 4) { SDDM_STRIP(2, 4) } else if (upt <= 8) { SDDM_STRIP(2, 8) } else { SDDM_STRIP(2, 16) }
-  }
-#undef SDDM_STRIP
+template <typename T, int FC, int W, int CIN>
+static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size_t* lo) {
+  const size_t lds = strip_lds<T, FC, W, CIN>(a);
+  if (lo) { *lo = lds; return hipSuccess; }
+  constexpr int TR = 128 / W;
+  if (lds > 160 * 1024 || a.Ho % SR || SR % TR) return hipErrorInvalidValue;
+  const int nz = (a.Cout + 16 * FC - 1) / (16 * FC);
+  hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN>), dim3(a.Ho / SR, B, nz), dim3(256), lds, s, a, SR);
   return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t strip_dispatch(const ConvArgs& a, int nblk, int SR, int B, hipStream_t s, size_t* lo) {
+  const int Cin = a.CA + a.CB;
+#define SDDM_STRIP(FCV, WV, CV) \
+  if (nblk == 16 * FCV && a.Wo == WV && Cin == CV) return strip_go<T, FCV, WV, CV>(a, SR, B, s, lo);
+  SDDM_STRIP(2, 128, 32) SDDM_STRIP(2, 128, 64) SDDM_STRIP(4, 128, 32) SDDM_STRIP(4, 128, 64)
+  SDDM_STRIP(2, 64, 32) SDDM_STRIP(2, 64, 64) SDDM_STRIP(2, 64, 128)
+  SDDM_STRIP(4, 64, 32) SDDM_STRIP(4, 64, 64) SDDM_STRIP(4, 64, 128)
+#undef SDDM_STRIP
+  if (lo) *lo = (size_t)1 << 40;
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_conv_strip(int dtype, int nblk, int SR, const ConvArgs& a, int B, hipStream_t s) {
@@ -320,7 +322,7 @@ hipError_t launch_conv_strip(int dtype, int nblk, int SR, const ConvArgs& a, int
 }
 
 size_t conv_strip_lds_bytes(int dtype, int nblk, const ConvArgs& a) {
-  size_t lo = 0;
+  size_t lo = (size_t)1 << 40;
   if (dtype == DT_F32) (void)strip_dispatch<float>(a, nblk, 1, 1, 0, &lo);
   else if (dtype == DT_BF16) (void)strip_dispatch<bf16_t>(a, nblk, 1, 1, 0, &lo);
   else (void)strip_dispatch<f16_t>(a, nblk, 1, 1, 0, &lo);

@@ -76,9 +76,10 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
         const T* src = fromA ? (const T*)a.srcA : (const T*)a.srcB;
         const int Cs = fromA ? a.CA : a.CB;
         const int cs0 = fromA ? c0 : c0 - a.CA;
+        const int rowu = HC * UPP;                 // units per halo row
+        int hy = tid / rowu, j = tid - hy * rowu;  // one division per thread, then incremental
         for (int u = tid; u < HR * HC * UPP; u += 256) {
-          const int hp = u / UPP, q = u - hp * UPP;
-          const int hy = hp / HC, hx = hp - hy * HC;
+          const int hx = j / UPP, q = j - hx * UPP, hp = hy * HC + hx;
           int iy, ix;
           bool ok;
           if (S2) {
@@ -92,10 +93,12 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
           f32x4 v = {0.f, 0.f, 0.f, 0.f};
           if (ok) {
             const size_t pi = (size_t)b * img_in + (size_t)iy * a.Wi + ix;
-            v = transform_vec<T>(*(const f32x4*)((const char*)(src + pi * Cs + cs0) + q * 16),
-                                 gsc + c0 + q * VE, gsc + Cin + c0 + q * VE, gn);
+            v = *(const f32x4*)((const char*)(src + pi * Cs + cs0) + q * 16);
+            if (gn) v = transform_fast<T>(v, gsc + c0 + q * VE, gsc + Cin + c0 + q * VE);
           }
           *(f32x4*)(slot + hp * PIX + q * 16) = v;
+          j += 256;
+          while (j >= rowu) { j -= rowu; ++hy; }
         }
       } else {   // raw 1x1 residual chunk: the MBLK centre pixels, untransformed
         const int c0 = (ck - nck) * CK;

@@ -83,6 +83,9 @@ struct TransCoef {            // device pointers to the GaussianDiffusion buffer
   const float* sigma; const float* sgamma; const float* ssh; const float* sqrt_delta;
   const float* c_xt; const float* c_yt; const float* c_epst; const float* sde;
 };
+struct StepParams { int t; int pad; uint64_t seed; int64_t row_offset; };   // device-side, per sample call
+hipError_t launch_set_params(StepParams* p, int t, uint64_t seed, int64_t row_offset, hipStream_t s);
+
 struct FinalArgs {
   const void* src; int C;     // [B][F][W][C] (T)
   const float* gst; int gtiles, gntile;          // producer tile statistics (final_conv GroupNorm)
@@ -96,6 +99,7 @@ struct FinalArgs {
   const int* t_dev;
   TransCoef co;
   uint64_t seed; int64_t row_offset;
+  const StepParams* sp;       // when set, seed / row_offset come from device memory (graph replay)
 };
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s);
 

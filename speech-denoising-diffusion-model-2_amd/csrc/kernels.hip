@@ -131,17 +131,15 @@ hipError_t launch_gn_finalize(const GNArgs& a, hipStream_t s) {
 // =============================================================================================
 template <typename T>
 __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* wl = (float*)smem;                 // [Cout][2][9] + bias
-  float* otile = wl + a.Cout * 18 + a.Cout; // [TR*W][Cout+1]
+  constexpr int CO = 32;                    // inner_channel (checked by the launcher)
+  __shared__ float otile[256 * (CO + 1)];   // [pixels][Cout+1] for the tile statistics
   const int b = blockIdx.y, f0 = blockIdx.x * a.TR, tid = threadIdx.x;
   if (a.t_dev && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.t_dev -= 1;
-  for (int i = tid; i < a.Cout * 18; i += blockDim.x) wl[i] = a.w[i];
-  for (int i = tid; i < a.Cout; i += blockDim.x) wl[a.Cout * 18 + i] = a.bias[i];
-  __syncthreads();
-  const int ld = a.Cout + 1, npix = a.TR * a.W;
+  const int npix = a.TR * a.W;
   const float* cnd = a.cond + (size_t)b * a.N;
   const float* xx = a.x + (size_t)b * a.N;
+  constexpr int VE = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(VE)));
   for (int p = tid; p < npix; p += blockDim.x) {
     const int f = f0 + p / a.W, w = p % a.W;
     float in0[9], in1[9];
@@ -155,31 +153,36 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
         in0[dy * 3 + dx] = ok ? cnd[n] : 0.f;
         in1[dy * 3 + dx] = ok ? xx[n] : 0.f;
       }
-    for (int co = 0; co < a.Cout; ++co) {
-      const float* wc = wl + co * 18;
-      float s = 0.f;
+    T* op = (T*)a.out + (((size_t)b * a.F + f) * a.W + w) * CO;
+    const float* __restrict__ wg = a.w;      // uniform addresses -> scalar loads, SGPR operands
+    const float* __restrict__ bg = a.bias;
+    for (int c0 = 0; c0 < CO; c0 += VE) {
+      vec v;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) s += wc[k] * in0[k];
+      for (int j = 0; j < VE; ++j) {
+        const float* wc = wg + (c0 + j) * 18;
+        float s = 0.f;
 #pragma unroll
-      for (int k = 0; k < 9; ++k) s += wc[9 + k] * in1[k];
-      s += wl[a.Cout * 18 + co];
-      otile[p * ld + co] = to_f32<T>(from_f32<T>(s));
+        for (int k = 0; k < 9; ++k) s += wc[k] * in0[k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) s += wc[9 + k] * in1[k];
+        s += bg[c0 + j];
+        v[j] = from_f32<T>(s);
+        if (p < 256) otile[p * (CO + 1) + c0 + j] = to_f32<T>(v[j]);
+      }
+      *(vec*)(op + c0) = v;
     }
   }
   __syncthreads();
-  // store NHWC rows (contiguous: TR*W pixels * Cout channels)
-  T* out = (T*)a.out + ((size_t)b * a.F + f0) * a.W * a.Cout;
-  for (int i = tid; i < npix * a.Cout; i += blockDim.x) out[i] = from_f32<T>(otile[(i / a.Cout) * ld + i % a.Cout]);
-  tile_channel_stats(otile, ld, npix, a.Cout,
-                     a.stats + ((size_t)b * (a.F / a.TR) + blockIdx.x) * a.Cout * 2, 2);
+  tile_channel_stats(otile, CO + 1, npix, CO, a.stats + ((size_t)b * (a.F / a.TR) + blockIdx.x) * CO * 2, 2);
 }
 
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s) {
-  const size_t lds = (size_t)(a.Cout * 19) * 4 + (size_t)a.TR * a.W * (a.Cout + 1) * 4;
+  if (a.Cout != 32 || a.TR * a.W != 256 || a.F % a.TR) return hipErrorInvalidValue;
   dim3 grid(a.F / a.TR, B);
-  if (dtype == DT_F32) hipLaunchKernelGGL(conv_in_kernel<float>, grid, dim3(256), lds, s, a);
-  else if (dtype == DT_BF16) hipLaunchKernelGGL(conv_in_kernel<bf16_t>, grid, dim3(256), lds, s, a);
-  else hipLaunchKernelGGL(conv_in_kernel<f16_t>, grid, dim3(256), lds, s, a);
+  if (dtype == DT_F32) hipLaunchKernelGGL(conv_in_kernel<float>, grid, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(conv_in_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(conv_in_kernel<f16_t>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -310,12 +313,14 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   const int t = a.t_dev ? *a.t_dev : 0;
   float* xrow = a.x + (size_t)b * a.N;
   const float* crow = a.cond ? a.cond + (size_t)b * a.N : nullptr;
-  const int64_t ebase = (a.row_offset + b) * (int64_t)a.N;
+  const uint64_t seed = a.sp ? a.sp->seed : a.seed;
+  const int64_t row_offset = a.sp ? a.sp->row_offset : a.row_offset;
+  const int64_t ebase = (row_offset + b) * (int64_t)a.N;
   for (int n4 = n_begin + 4 * tid; n4 < n_end; n4 += 4 * blockDim.x) {
     const uint64_t e0 = (uint64_t)(ebase + n4);
     f32x4 z = {0.f, 0.f, 0.f, 0.f};
     const bool aligned = (e0 & 3) == 0;
-    if (a.mode >= 0 && t > 1 && aligned) z = philox_normal4(a.seed, (uint32_t)t, e0 >> 2);
+    if (a.mode >= 0 && t > 1 && aligned) z = philox_normal4(seed, (uint32_t)t, e0 >> 2);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int n = n4 + j;
@@ -328,7 +333,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
       if (a.mode < 0) {
         a.eps_out[(size_t)b * a.N + n] = e;
       } else {
-        const float zz = (t > 1) ? (aligned ? z[j] : philox_normal1(a.seed, (uint32_t)t, e0 + j)) : 0.f;
+        const float zz = (t > 1) ? (aligned ? z[j] : philox_normal1(seed, (uint32_t)t, e0 + j)) : 0.f;
         xrow[n] = transition_one(a.mode, a.co, t, xrow[n], e, crow ? crow[n] : 0.f, zz);
       }
     }
@@ -359,6 +364,13 @@ hipError_t launch_init_state(const InitArgs& a, hipStream_t s) {
 }
 
 __global__ void set_int_kernel(int* p, int v) { *p = v; }
+__global__ void set_params_kernel(StepParams* p, int t, uint64_t seed, int64_t row_offset) {
+  p->t = t; p->seed = seed; p->row_offset = row_offset;
+}
+hipError_t launch_set_params(StepParams* p, int t, uint64_t seed, int64_t row_offset, hipStream_t s) {
+  hipLaunchKernelGGL(set_params_kernel, dim3(1), dim3(1), 0, s, p, t, seed, row_offset);
+  return hipGetLastError();
+}
 hipError_t launch_set_int(int* p, int v, hipStream_t s) {
   hipLaunchKernelGGL(set_int_kernel, dim3(1), dim3(1), 0, s, p, v);
   return hipGetLastError();

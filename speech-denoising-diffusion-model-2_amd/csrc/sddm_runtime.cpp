@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdarg>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <functional>
@@ -240,6 +241,15 @@ struct sddm_ctx {
   std::vector<Op> ops;
   size_t off_temb_fwd = 0, off_nl = 0;
   RunState rs;
+  size_t off_cond = 0, off_x = 0;   // graph-stable copies of cond / x_t
+  int plan_gen = 0;
+  // graph replay of K steps on a private stream
+  hipStream_t work = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  int g_K = 0, g_gen = -1;
+  bool use_graphs = true;
   // profiling
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
@@ -480,6 +490,8 @@ static int build_plan(sddm_ctx* c, int B) {
     return (int)gres.size() - 1;
   };
   c->off_temb_fwd = A.reserve(sizeof(float) * (size_t)B * std::max(c->SC, 1));
+  c->off_cond = A.reserve(sizeof(float) * (size_t)B * N);
+  c->off_x = A.reserve(sizeof(float) * (size_t)B * N);
   c->off_nl = A.reserve(sizeof(float) * B);
 
   enum { ST_CONVIN, ST_GN, ST_CONV, ST_FINAL };
@@ -496,8 +508,9 @@ static int build_plan(sddm_ctx* c, int B) {
   auto pick = [&](int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up, ConvChoice& ch) {
     return choose_conv(dt, B, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch);
   };
-  const int TRin = 2;
-  if (F % TRin) FAIL(SDDM_ERR_SHAPE, "n_frames %d not even", F);
+  const int TRin = 256 / W;
+  if (u.inner != 32 || 256 % W || F % TRin)
+    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "conv_in needs inner_channel 32 and segment_len dividing 256 (got %d, %d)", u.inner, W);
   const int t0 = new_tensor(u.inner, F, W, F / TRin, TRin * W);
   { Step st; st.type = ST_CONVIN; st.out = t0; prog.push_back(st); }
 
@@ -663,11 +676,13 @@ static int build_plan(sddm_ctx* c, int B) {
                           x.mode = ctx->rs.final_mode; x.eps_out = ctx->rs.eps_out;
                           x.x = ctx->rs.x; x.cond = ctx->rs.cond; x.t_dev = ctx->rs.t_dev;
                           x.seed = ctx->rs.seed; x.row_offset = ctx->rs.row_offset;
+                          x.sp = ctx->rs.t_dev ? (const StepParams*)ctx->rs.t_dev : nullptr;
                           return launch_final(dt, x, B, s);
                         }, "final_conv"});
     }
   }
   c->plan_B = B;
+  c->plan_gen++;
   return SDDM_OK;
 }
 
@@ -726,6 +741,7 @@ int sddm_create(int device, int compute_dtype, sddm_ctx** out) {
   sddm_ctx* c = new sddm_ctx();
   c->device = device;
   c->dtype = compute_dtype;
+  c->use_graphs = std::getenv("SDDM_NO_GRAPH") == nullptr;
   *out = c;
   return SDDM_OK;
 }
@@ -733,6 +749,11 @@ int sddm_create(int device, int compute_dtype, sddm_ctx** out) {
 void sddm_destroy(sddm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
+  if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
+  if (c->graph) (void)hipGraphDestroy(c->graph);
+  if (c->work) { (void)hipStreamSynchronize(c->work); (void)hipStreamDestroy(c->work); }
+  if (c->ev_in) (void)hipEventDestroy(c->ev_in);
+  if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->aarena.reset();
   c->warena.reset();
@@ -926,10 +947,29 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
   if (!cond || !out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
   r = prepare_plan(c, B, N);
   if (r) return r;
-  hipStream_t s = (hipStream_t)stream;
+  hipStream_t user = (hipStream_t)stream;
+  const bool graph = c->use_graphs && !c->prof && !record;
+  hipStream_t s = user;
+  if (graph) {
+    if (!c->work) {
+      SDDM_HIP_CHECK(hipStreamCreateWithFlags(&c->work, hipStreamNonBlocking));
+      SDDM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+      SDDM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
+    }
+    SDDM_HIP_CHECK(hipEventRecord(c->ev_in, user));
+    SDDM_HIP_CHECK(hipStreamWaitEvent(c->work, c->ev_in, 0));
+    s = c->work;
+  }
   const int T = c->T;
-  int* t_dev = c->warena.at<int>(c->off_tdev);
+  StepParams* sp = c->warena.at<StepParams>(c->off_tdev);
+  int* t_dev = &sp->t;
   float* temb_tab = c->warena.at<float>(c->off_temb_tab);
+  float* xb = graph ? c->aarena.at<float>(c->off_x) : out;
+  const float* cb = cond;
+  if (graph) {
+    SDDM_HIP_CHECK(hipMemcpyAsync(c->aarena.at<float>(c->off_cond), cond, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
+    cb = c->aarena.at<float>(c->off_cond);
+  }
   // noise-level embeddings of every t (same for all rows: model.py:108)
   EmbedArgs e{};
   e.table = c->dtab(3); e.time_step_mode = c->noise_time_step; e.R = T + 1; e.dim = c->ucfg.inner;
@@ -940,18 +980,46 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
   e.SC = c->SC; e.out = temb_tab;
   SDDM_HIP_CHECK(launch_embed(e, s));
   InitArgs ia{};
-  ia.mode = c->init_mode; ia.cond = cond; ia.out = out; ia.total = B * N; ia.N = N; ia.T = T;
+  ia.mode = c->init_mode; ia.cond = cb; ia.out = xb; ia.total = B * N; ia.N = N; ia.T = T;
   ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset;
   SDDM_HIP_CHECK(launch_init_state(ia, s));
-  SDDM_HIP_CHECK(launch_set_int(t_dev, T + 1, s));
-  c->rs.cond = cond; c->rs.x = out; c->rs.temb = temb_tab; c->rs.temb_per_b = 0; c->rs.t_dev = t_dev;
+  SDDM_HIP_CHECK(launch_set_params(sp, T + 1, seed, row_offset, s));
+  c->rs.cond = cb; c->rs.x = xb; c->rs.temb = temb_tab; c->rs.temb_per_b = 0; c->rs.t_dev = t_dev;
   c->rs.final_mode = c->tr_mode; c->rs.eps_out = nullptr; c->rs.seed = seed; c->rs.row_offset = row_offset;
+  if (graph) {
+    int K = 1;
+    for (int k : {10, 8, 5, 4, 2})
+      if (T % k == 0) { K = k; break; }
+    if (!c->gexec || c->g_gen != c->plan_gen || c->g_K != K) {
+      if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
+      if (c->graph) { (void)hipGraphDestroy(c->graph); c->graph = nullptr; }
+      SDDM_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+      for (int k = 0; k < K; ++k) {
+        r = run_ops(c, s);
+        if (r) {
+          hipGraph_t junk = nullptr;
+          (void)hipStreamEndCapture(s, &junk);
+          if (junk) (void)hipGraphDestroy(junk);
+          return r;
+        }
+      }
+      SDDM_HIP_CHECK(hipStreamEndCapture(s, &c->graph));
+      SDDM_HIP_CHECK(hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
+      c->g_gen = c->plan_gen;
+      c->g_K = K;
+    }
+    for (int i = 0; i < T / K; ++i) SDDM_HIP_CHECK(hipGraphLaunch(c->gexec, s));
+    SDDM_HIP_CHECK(hipMemcpyAsync(out, xb, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
+    SDDM_HIP_CHECK(hipEventRecord(c->ev_out, s));
+    SDDM_HIP_CHECK(hipStreamWaitEvent(user, c->ev_out, 0));
+    return SDDM_OK;
+  }
   int64_t nrec = 0;
   for (int t = T; t >= 1; --t) {
     r = run_ops(c, s);
     if (r) return r;
     if (record && t % sample_inter == 0) {  // model.py:100-101: keep x_{t-1} when t % inter == 0
-      SDDM_HIP_CHECK(hipMemcpyAsync(record + nrec * B * N, out, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
+      SDDM_HIP_CHECK(hipMemcpyAsync(record + nrec * B * N, xb, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
       ++nrec;
     }
   }
