@@ -6,8 +6,9 @@
 //   * the weight slab of its channel tile (loaded once per strip, not once per tile), and
 //   * a ring of R = 2*TR + 2 transformed input rows (GroupNorm + SiLU applied once per element,
 //     zero halo columns, nearest-2x upsample / channel concat resolved while loading),
-// and walks the strip TR = 128 / W output rows at a time (128 pixels = 4 waves x 2 MFMA column
-// fragments).  While the MFMAs of iteration i run on rows [y-1, y+TR] of the ring, each thread
+// and walks the strip TR = MPI / W output rows at a time (MPI = 128 or 256 pixels, one wave per
+// 32 pixels = 2 MFMA column fragments; with MPI = 256 each SIMD runs two waves, so one wave's
+// GN+SiLU staging overlaps the other's MFMAs).  While the MFMAs of iteration i run on rows [y-1, y+TR] of the ring, each thread
 // already holds in registers the raw input of rows [y+TR+1, y+2TR] (issued before the MFMAs) and
 // writes them transformed into the free ring slots afterwards: one barrier per iteration.
 //
@@ -25,11 +26,13 @@
 
 namespace sddm {
 
-template <typename T, int FC, int W, int CIN>
-__global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
+template <typename T, int FC, int W, int CIN, int MPI>
+__global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR) {
+  constexpr int NT = MPI * 2;                     // threads: one wave per 32 pixels of an iteration
+  constexpr int NWV = NT / 64;
   constexpr int ES = (int)sizeof(T);
   constexpr int NBLK = 16 * FC, FP = 2;
-  constexpr int TR = 128 / W, R = 2 * TR + 2;
+  constexpr int TR = MPI / W, R = 2 * TR + 2;
   constexpr int UPP = CIN * ES / 16;              // 16-byte channel units (planes) per pixel
   constexpr int UPL = ES / 2;                     // units per lane group (8 channels)
   constexpr int VE = 16 / ES;
@@ -40,9 +43,9 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
   constexpr int WPLANES = NCK * 9 * 4 * UPL;
   constexpr int PB = 64 / UPP;                    // pixels per 64-unit staging group
   constexpr int NU = TR * W * UPP;                // units of TR rows
-  constexpr int UPT = NU / 256;                   // prefetch units per thread
+  constexpr int UPT = NU / NT;                    // prefetch units per thread
   static_assert(UPP >= 1 && UPP <= 64 && (64 % UPP) == 0, "channel units must divide a wave");
-  static_assert(NU % 256 == 0, "prefetch must split evenly");
+  static_assert(NU % NT == 0, "prefetch must split evenly");
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
@@ -57,7 +60,7 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
   char* rw = wl + WPLANES * WPL;                  // [RC*ES/16 planes][NBLK][16 B]
   const int RPLANES = res2 ? RC * ES / 16 : 0;
   float* gsc = (float*)(rw + RPLANES * WPL);      // [2][CIN]
-  float* red = gsc + 2 * CIN;                     // [4 waves][NBLK][3]
+  float* red = gsc + 2 * CIN;                     // [NWV waves][NBLK][3]
 
   const int y0 = strip * SR;
   // ---------------- prologue ----------------
@@ -65,19 +68,19 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
     const GNFuse f{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
     gn_fused_prologue(f, b, a.CA, a.CB, gsc, gsc + CIN);
   }
-  for (int u = tid; u < NBLK * WPLANES; u += 256) {       // co fastest: conflict-free LDS writes
+  for (int u = tid; u < NBLK * WPLANES; u += NT) {        // co fastest: conflict-free LDS writes
     const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
     const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
     *(f32x4*)(wl + pl * WPL + co * 16) =
         *(const f32x4*)((const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16);
   }
   if (res2) {
-    for (int u = tid; u < NBLK * RPLANES; u += 256) {
+    for (int u = tid; u < NBLK * RPLANES; u += NT) {
       const int co = u % NBLK, pl = u / NBLK;
       *(f32x4*)(rw + pl * WPL + co * 16) = *(const f32x4*)((const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16);
     }
   }
-  for (int u = tid; u < R * UPP * 2; u += 256) {          // zero halo columns
+  for (int u = tid; u < R * UPP * 2; u += NT) {           // zero halo columns
     const int side = u & 1, pl = u >> 1;
     *(f32x4*)(ring + pl * PL + (side ? (W + 1) : 0) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
   const int base = ((y0 - 1) % R + R) % R;                 // ring slot of row y0 - 1
 
   // initial rows y0-1 .. y0+TR
-  for (int u = tid; u < (TR + 2) * W * UPP; u += 256) {
+  for (int u = tid; u < (TR + 2) * W * UPP; u += NT) {
     const int grp = u >> 6, j = u & 63;
     const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
     const int ry = y0 - 1 + r;
@@ -108,19 +111,29 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
   int prow[FP], pcol[FP];
 #pragma unroll
   for (int fp = 0; fp < FP; ++fp) {
-    const int p = wave * 32 + fp * 16 + (lane & 15);
+    const int p = wave * 32 + fp * 16 + (lane & 15);   // pixel inside the MPI-pixel iteration
     prow[fp] = p / W;
     pcol[fp] = p % W;
   }
-  // prefetch geometry of this thread's units (same every iteration)
+  // prefetch geometry of this thread's units (same every iteration): source pointer of row 0
+  // (column and channel offset folded in) and the unit's row inside the TR-row group
   int pr[UPT], px[UPT], pq[UPT];
+  const char* ubase[UPT];
+  int ustride[UPT];
 #pragma unroll
   for (int k = 0; k < UPT; ++k) {
-    const int u = tid + k * 256, grp = u >> 6, j = u & 63;
+    const int u = tid + k * NT, grp = u >> 6, j = u & 63;
     const int pix = grp * PB + (j % PB);
     pq[k] = j / PB;
     pr[k] = pix / W;
     px[k] = pix % W;
+    const int c0 = pq[k] * VE;
+    const int sx = a.upsample ? (px[k] >> 1) : px[k];
+    const bool fa = c0 < a.CA;
+    const int Cs = fa ? a.CA : a.CB;
+    ubase[k] = (const char*)((fa ? (const T*)a.srcA : (const T*)a.srcB) +
+                             (((size_t)b * a.Hi) * a.Wi + sx) * Cs + (fa ? c0 : c0 - a.CA));
+    ustride[k] = a.Wi * Cs * ES;                           // bytes per source row
   }
   float sK[FC][4], s1[FC][4], s2[FC][4];
 #pragma unroll
@@ -149,7 +162,11 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
     const bool do_pre = it + 1 < iters;
     if (do_pre) {
 #pragma unroll
-      for (int k = 0; k < UPT; ++k) pre[k] = load_unit(y + TR + 1 + pr[k], px[k], pq[k]);
+      for (int k = 0; k < UPT; ++k) {
+        const int ry = y + TR + 1 + pr[k];
+        const int sy = a.upsample ? (ry >> 1) : ry;
+        pre[k] = ry < H ? *(const f32x4*)(ubase[k] + sy * ustride[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     }
     // ---- MFMA over the 9 taps x CIN/32 chunks of the current rows ----
     f32x4 acc[FP][FC];
@@ -267,7 +284,7 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
     __syncthreads();
     if (tid < NBLK && n0 + tid < a.Cout) {
       float n = 0.f, mean = 0.f, m2 = 0.f;
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NWV; ++w) {
         const float* rr = red + (w * NBLK + tid) * 3;
         const float nb = rr[0], d = rr[1] - mean, nt = n + nb;
         mean += d * nb / nt;
@@ -281,32 +298,34 @@ __global__ __launch_bounds__(256) void conv_strip_kernel(ConvArgs a, int SR) {
   }
 }
 
-template <typename T, int FC, int W, int CIN>
+template <typename T, int FC, int W, int CIN, int MPI>
 static size_t strip_lds(const ConvArgs& a) {
-  constexpr int ES = (int)sizeof(T), NBLK = 16 * FC, TR = 128 / W, R = 2 * TR + 2;
+  constexpr int ES = (int)sizeof(T), NBLK = 16 * FC, TR = MPI / W, R = 2 * TR + 2;
   constexpr int UPP = CIN * ES / 16, PL = ((W + 2) * 16 + 255) / 256 * 256;
   size_t n = (size_t)R * UPP * PL + (size_t)(CIN / 32) * 9 * 4 * (ES / 2) * NBLK * 16;
   if (a.res_mode == 2) n += (size_t)((a.RCA + a.RCB) * ES / 16) * NBLK * 16;
-  n += (size_t)2 * CIN * 4 + (size_t)4 * NBLK * 3 * 4;
+  n += (size_t)2 * CIN * 4 + (size_t)(MPI / 32) * NBLK * 3 * 4;
   return n;
 }
 
-template <typename T, int FC, int W, int CIN>
+template <typename T, int FC, int W, int CIN, int MPI>
 static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size_t* lo) {
-  const size_t lds = strip_lds<T, FC, W, CIN>(a);
+  const size_t lds = strip_lds<T, FC, W, CIN, MPI>(a);
   if (lo) { *lo = lds; return hipSuccess; }
-  constexpr int TR = 128 / W;
+  constexpr int TR = MPI / W;
   if (lds > 160 * 1024 || a.Ho % SR || SR % TR) return hipErrorInvalidValue;
   const int nz = (a.Cout + 16 * FC - 1) / (16 * FC);
-  hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN>), dim3(a.Ho / SR, B, nz), dim3(256), lds, s, a, SR);
+  hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI>), dim3(a.Ho / SR, B, nz), dim3(MPI * 2), lds, s, a, SR);
   return hipGetLastError();
 }
 
+// mpi: pixels per iteration (128 -> 4 waves, 256 -> 8 waves = two per SIMD)
 template <typename T>
-static hipError_t strip_dispatch(const ConvArgs& a, int nblk, int SR, int B, hipStream_t s, size_t* lo) {
+static hipError_t strip_dispatch(const ConvArgs& a, int nblk, int mpi, int SR, int B, hipStream_t s, size_t* lo) {
   const int Cin = a.CA + a.CB;
-#define SDDM_STRIP(FCV, WV, CV) \
-  if (nblk == 16 * FCV && a.Wo == WV && Cin == CV) return strip_go<T, FCV, WV, CV>(a, SR, B, s, lo);
+#define SDDM_STRIP(FCV, WV, CV)                                                                   \
+  if (nblk == 16 * FCV && a.Wo == WV && Cin == CV)                                                \
+    return mpi == 256 ? strip_go<T, FCV, WV, CV, 256>(a, SR, B, s, lo) : strip_go<T, FCV, WV, CV, 128>(a, SR, B, s, lo);
   SDDM_STRIP(2, 128, 32) SDDM_STRIP(2, 128, 64) SDDM_STRIP(4, 128, 32) SDDM_STRIP(4, 128, 64)
   SDDM_STRIP(2, 64, 32) SDDM_STRIP(2, 64, 64) SDDM_STRIP(2, 64, 128)
   SDDM_STRIP(4, 64, 32) SDDM_STRIP(4, 64, 64) SDDM_STRIP(4, 64, 128)
@@ -315,17 +334,17 @@ static hipError_t strip_dispatch(const ConvArgs& a, int nblk, int SR, int B, hip
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_conv_strip(int dtype, int nblk, int SR, const ConvArgs& a, int B, hipStream_t s) {
-  if (dtype == DT_F32) return strip_dispatch<float>(a, nblk, SR, B, s, nullptr);
-  if (dtype == DT_BF16) return strip_dispatch<bf16_t>(a, nblk, SR, B, s, nullptr);
-  return strip_dispatch<f16_t>(a, nblk, SR, B, s, nullptr);
+hipError_t launch_conv_strip(int dtype, int nblk, int mpi, int SR, const ConvArgs& a, int B, hipStream_t s) {
+  if (dtype == DT_F32) return strip_dispatch<float>(a, nblk, mpi, SR, B, s, nullptr);
+  if (dtype == DT_BF16) return strip_dispatch<bf16_t>(a, nblk, mpi, SR, B, s, nullptr);
+  return strip_dispatch<f16_t>(a, nblk, mpi, SR, B, s, nullptr);
 }
 
-size_t conv_strip_lds_bytes(int dtype, int nblk, const ConvArgs& a) {
+size_t conv_strip_lds_bytes(int dtype, int nblk, int mpi, const ConvArgs& a) {
   size_t lo = (size_t)1 << 40;
-  if (dtype == DT_F32) (void)strip_dispatch<float>(a, nblk, 1, 1, 0, &lo);
-  else if (dtype == DT_BF16) (void)strip_dispatch<bf16_t>(a, nblk, 1, 1, 0, &lo);
-  else (void)strip_dispatch<f16_t>(a, nblk, 1, 1, 0, &lo);
+  if (dtype == DT_F32) (void)strip_dispatch<float>(a, nblk, mpi, 1, 1, 0, &lo);
+  else if (dtype == DT_BF16) (void)strip_dispatch<bf16_t>(a, nblk, mpi, 1, 1, 0, &lo);
+  else (void)strip_dispatch<f16_t>(a, nblk, mpi, 1, 1, 0, &lo);
   return lo;
 }
 

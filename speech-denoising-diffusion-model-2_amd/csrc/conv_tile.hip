@@ -14,7 +14,7 @@
 
 namespace sddm {
 
-template <typename T, bool S2, int KW, int FP, int FC>
+template <typename T, bool S2, int KW, int FP, int FC, int MAXU>
 __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
   constexpr int WM = 4 / KW;
   constexpr int ES = (int)sizeof(T);
@@ -63,22 +63,157 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
 
   const size_t img_in = (size_t)a.Hi * a.Wi;
   const int rounds = (nall + KW - 1) / KW;
+  const int halo_units = HR * HC * UPP;             // units of one 3x3 chunk
   for (int rd = 0; rd < rounds; ++rd) {
-    __syncthreads();   // previous round's readers done (and gsc written on the first round)
-    // ---- stage chunks rd*KW .. rd*KW+KW-1 (all 256 threads) ----
-    for (int s = 0; s < KW; ++s) {
+    // ---- 1. this wave's weight fragments for the whole chunk (latency overlaps the staging) ----
+    const int myck = rd * KW + wk;
+    constexpr bool PRE = KW > 1;       // K-split blocks are few: hide the weight latency behind staging
+    constexpr int NW = PRE ? 9 : 1;
+    Frag<T> wf[NW][FC];
+    if (PRE && myck < nck) {
+      const T* wrow = (const T*)a.wgt + ((size_t)(n0 + (lane & 15)) * nck + myck) * 9 * CK + g * 8;
+      const size_t fstride = (size_t)16 * nck * 9 * CK;   // 16 output channels
+#pragma unroll
+      for (int tap = 0; tap < NW; ++tap)
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) wf[tap][fc] = load_frag<T>((const char*)(wrow + fc * fstride + tap * CK));
+    } else if (myck >= nck && myck < nall) {
+      const int c0 = (myck - nck) * CK;
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc)
+        wf[0][fc] = load_frag<T>((const char*)((const T*)a.res_wgt + (size_t)(n0 + fc * 16 + (lane & 15)) * RC + c0 + g * 8));
+    }
+    if constexpr (PRE) {
+    // ---- 2. batched staging loads of chunks rd*KW .. rd*KW+KW-1 (all 256 threads) ----
+    const int nst = min(KW, nall - rd * KW);
+    int total = 0;
+    for (int s = 0; s < nst; ++s) total += (rd * KW + s < nck) ? halo_units : MBLK * UPP;
+    f32x4 reg[MAXU];
+    int dst[MAXU];                                    // LDS byte offset, -1 = nothing
+    int gsel[MAXU];                                   // channel offset for the GN affine, -1 = no transform
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      const int u = tid + k * 256;
+      dst[k] = -1;
+      gsel[k] = -1;
+      reg[k] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (u >= total) continue;
+      int s = 0, v = u;
+      while (s < nst) {
+        const int n = (rd * KW + s < nck) ? halo_units : MBLK * UPP;
+        if (v < n) break;
+        v -= n;
+        ++s;
+      }
       const int ck = rd * KW + s;
-      if (ck >= nall) break;
       char* slot = stage + s * slot_bytes;
+      if (ck < nck) {
+        const int c0 = ck * CK;
+        const int hp = v / UPP, q = v - hp * UPP;
+        const int hy = hp / HC, hx = hp - hy * HC;
+        int iy, ix;
+        bool ok;
+        if (S2) {
+          iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
+          ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+        } else {
+          iy = y0 - 1 + hy; ix = x0 - 1 + hx;
+          ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
+          if (a.upsample) { iy >>= 1; ix >>= 1; }
+        }
+        dst[k] = (int)(slot - smem) + hp * PIX + q * 16;
+        if (ok) {
+          const bool fromA = c0 < a.CA;
+          const T* src = fromA ? (const T*)a.srcA : (const T*)a.srcB;
+          const int Cs = fromA ? a.CA : a.CB;
+          const size_t pi = (size_t)b * img_in + (size_t)iy * a.Wi + ix;
+          reg[k] = *(const f32x4*)((const char*)(src + pi * Cs + (fromA ? c0 : c0 - a.CA)) + q * 16);
+          gsel[k] = c0 + q * VE;
+        }
+      } else {
+        const int c0 = (ck - nck) * CK;
+        const int p = v / UPP, q = v - p * UPP;
+        dst[k] = (int)(slot - smem) + p * PIX + q * 16;
+        if (p < npix_valid) {
+          const bool fromA = c0 < a.RCA;
+          const T* src = fromA ? (const T*)a.rawA : (const T*)a.rawB;
+          const int Cs = fromA ? a.RCA : a.RCB;
+          const int py = p / a.TW, px = p - py * a.TW;
+          const size_t pi = ((size_t)b * a.Ho + (y0 + py)) * a.Wo + (x0 + px);
+          reg[k] = *(const f32x4*)((const char*)(src + pi * Cs + (fromA ? c0 : c0 - a.RCA)) + q * 16);
+        }
+      }
+    }
+    __syncthreads();   // previous round's readers done (and gsc written on the first round)
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      if (dst[k] < 0) continue;
+      f32x4 v = reg[k];
+      if (gn && gsel[k] >= 0) v = transform_fast<T>(v, gsc + gsel[k], gsc + Cin + gsel[k]);
+      *(f32x4*)(smem + dst[k]) = v;
+    }
+    for (int u = tid + MAXU * 256; u < total; u += 256) {   // overflow (never for the planned shapes)
+      int s = 0, v = u;
+      while (s < nst) {
+        const int n = (rd * KW + s < nck) ? halo_units : MBLK * UPP;
+        if (v < n) break;
+        v -= n;
+        ++s;
+      }
+      const int ck = rd * KW + s;
+      char* slot = stage + s * slot_bytes;
+      if (ck < nck) {
+        const int c0 = ck * CK, hp = v / UPP, q = v - hp * UPP, hy = hp / HC, hx = hp - hy * HC;
+        int iy, ix;
+        bool ok;
+        if (S2) {
+          iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
+          ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+        } else {
+          iy = y0 - 1 + hy; ix = x0 - 1 + hx;
+          ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
+          if (a.upsample) { iy >>= 1; ix >>= 1; }
+        }
+        f32x4 val = {0.f, 0.f, 0.f, 0.f};
+        if (ok) {
+          const bool fromA = c0 < a.CA;
+          const T* src = fromA ? (const T*)a.srcA : (const T*)a.srcB;
+          const int Cs = fromA ? a.CA : a.CB;
+          const size_t pi = (size_t)b * img_in + (size_t)iy * a.Wi + ix;
+          val = *(const f32x4*)((const char*)(src + pi * Cs + (fromA ? c0 : c0 - a.CA)) + q * 16);
+          if (gn) val = transform_fast<T>(val, gsc + c0 + q * VE, gsc + Cin + c0 + q * VE);
+        }
+        *(f32x4*)(slot + hp * PIX + q * 16) = val;
+      } else {
+        const int c0 = (ck - nck) * CK, p = v / UPP, q = v - p * UPP;
+        f32x4 val = {0.f, 0.f, 0.f, 0.f};
+        if (p < npix_valid) {
+          const bool fromA = c0 < a.RCA;
+          const T* src = fromA ? (const T*)a.rawA : (const T*)a.rawB;
+          const int Cs = fromA ? a.RCA : a.RCB;
+          const int py = p / a.TW, px = p - py * a.TW;
+          const size_t pi = ((size_t)b * a.Ho + (y0 + py)) * a.Wo + (x0 + px);
+          val = *(const f32x4*)((const char*)(src + pi * Cs + (fromA ? c0 : c0 - a.RCA)) + q * 16);
+        }
+        *(f32x4*)(slot + p * PIX + q * 16) = val;
+      }
+    }
+    __syncthreads();
+    } else {
+    // ---- 2'. streaming staging (KW == 1: many resident blocks hide the latency, keep VGPRs low) ----
+    __syncthreads();
+    {
+      const int ck = rd;
+      char* slot = stage;
       if (ck < nck) {
         const int c0 = ck * CK;
         const bool fromA = c0 < a.CA;
         const T* src = fromA ? (const T*)a.srcA : (const T*)a.srcB;
         const int Cs = fromA ? a.CA : a.CB;
         const int cs0 = fromA ? c0 : c0 - a.CA;
-        const int rowu = HC * UPP;                 // units per halo row
-        int hy = tid / rowu, j = tid - hy * rowu;  // one division per thread, then incremental
-        for (int u = tid; u < HR * HC * UPP; u += 256) {
+        const int rowu = HC * UPP;
+        int hy = tid / rowu, j = tid - hy * rowu;
+        for (int u = tid; u < halo_units; u += 256) {
           const int hx = j / UPP, q = j - hx * UPP, hp = hy * HC + hx;
           int iy, ix;
           bool ok;
@@ -100,7 +235,7 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
           j += 256;
           while (j >= rowu) { j -= rowu; ++hy; }
         }
-      } else {   // raw 1x1 residual chunk: the MBLK centre pixels, untransformed
+      } else {
         const int c0 = (ck - nck) * CK;
         const bool fromA = c0 < a.RCA;
         const T* src = fromA ? (const T*)a.rawA : (const T*)a.rawB;
@@ -119,20 +254,21 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
-    // ---- this wave's chunk ----
-    const int ck = rd * KW + wk;
-    if (ck < nall) {
+    }
+    // ---- 3. this wave's chunk ----
+    if (myck < nall) {
       const char* slot = stage + wk * slot_bytes;
-      if (ck < nck) {
-        const T* wrow = (const T*)a.wgt + ((size_t)(n0 + (lane & 15)) * nck + ck) * 9 * CK + g * 8;
-        const size_t fstride = (size_t)16 * nck * 9 * CK;   // 16 output channels
+      if (myck < nck) {
+        const T* wrow = (const T*)a.wgt + ((size_t)(n0 + (lane & 15)) * nck + myck) * 9 * CK + g * 8;
+        const size_t fstride = (size_t)16 * nck * 9 * CK;
 #pragma unroll
         for (int tap = 0; tap < 9; ++tap) {
           const int dy = tap / 3, dx = tap - 3 * dy;
           const int toff = (dy * HC + dx) * PIX;
           Frag<T> af[FC];
 #pragma unroll
-          for (int fc = 0; fc < FC; ++fc) af[fc] = load_frag<T>((const char*)(wrow + fc * fstride + tap * CK));
+          for (int fc = 0; fc < FC; ++fc)
+            af[fc] = PRE ? wf[PRE ? tap : 0][fc] : load_frag<T>((const char*)(wrow + fc * fstride + tap * CK));
 #pragma unroll
           for (int fp = 0; fp < FP; ++fp) {
             const Frag<T> bf = load_frag<T>(slot + pix_off[fp] + toff);
@@ -141,16 +277,11 @@ __global__ __launch_bounds__(256) void conv_tile_kernel(ConvArgs a) {
           }
         }
       } else {
-        const int c0 = (ck - nck) * CK;
-        Frag<T> af[FC];
-#pragma unroll
-        for (int fc = 0; fc < FC; ++fc)
-          af[fc] = load_frag<T>((const char*)((const T*)a.res_wgt + (size_t)(n0 + fc * 16 + (lane & 15)) * RC + c0 + g * 8));
 #pragma unroll
         for (int fp = 0; fp < FP; ++fp) {
           const Frag<T> bf = load_frag<T>(slot + pix_lin[fp]);
 #pragma unroll
-          for (int fc = 0; fc < FC; ++fc) mfma_frag(acc[fp][fc], af[fc], bf);
+          for (int fc = 0; fc < FC; ++fc) mfma_frag(acc[fp][fc], wf[0][fc], bf);
         }
       }
     }
@@ -221,7 +352,15 @@ static hipError_t tile_launch(const ConvArgs& a, int B, hipStream_t s, size_t* l
   if (lo) { *lo = lds; return hipSuccess; }
   if (lds > 160 * 1024) return hipErrorInvalidValue;
   const int nz = (a.Cout + FC * 16 - 1) / (FC * 16);
-  hipLaunchKernelGGL((conv_tile_kernel<T, S2, KW, FP, FC>), dim3(a.n_tiles, B, nz), dim3(256), lds, s, a);
+  // staging units per round -> register array size
+  constexpr int UPP = 32 * (int)sizeof(T) / 16;
+  const int HR = S2 ? 2 * a.TR + 1 : a.TR + 2, HC = S2 ? 2 * a.TW + 1 : a.TW + 2;
+  const int units = KW * HR * HC * UPP;
+  const int per = (units + 255) / 256;
+  const dim3 grid(a.n_tiles, B, nz);
+  if (per <= 4) hipLaunchKernelGGL((conv_tile_kernel<T, S2, KW, FP, FC, 4>), grid, dim3(256), lds, s, a);
+  else if (per <= 8) hipLaunchKernelGGL((conv_tile_kernel<T, S2, KW, FP, FC, 8>), grid, dim3(256), lds, s, a);
+  else hipLaunchKernelGGL((conv_tile_kernel<T, S2, KW, FP, FC, 16>), grid, dim3(256), lds, s, a);
   return hipGetLastError();
 }
 

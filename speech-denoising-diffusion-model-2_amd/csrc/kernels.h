@@ -74,8 +74,8 @@ hipError_t launch_conv3x3(int dtype, const ConvCfg& cfg, const ConvArgs& a, int 
 size_t conv3x3_lds_bytes(int dtype, const ConvCfg& cfg, const ConvArgs& a);
 
 // ---- row-streaming 3x3 convolution for segment widths 64 / 128 (conv_strip.hip) ----
-hipError_t launch_conv_strip(int dtype, int nblk, int SR, const ConvArgs& a, int B, hipStream_t s);
-size_t conv_strip_lds_bytes(int dtype, int nblk, const ConvArgs& a);
+hipError_t launch_conv_strip(int dtype, int nblk, int mpi, int SR, const ConvArgs& a, int B, hipStream_t s);
+size_t conv_strip_lds_bytes(int dtype, int nblk, int mpi, const ConvArgs& a);
 
 // ---- final Block(C -> 1) + overlapAdd + p_transition (UNetModified2.py:235,267-268; diffusion.py:164-223) ----
 struct TransCoef {            // device pointers to the GaussianDiffusion buffers [T+1]

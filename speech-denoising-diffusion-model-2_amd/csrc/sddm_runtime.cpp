@@ -425,7 +425,7 @@ static int choose_conv_cfg(int dt, int B, ConvArgs& a, ConvCfg& cfg, bool s2) {
 struct ConvChoice {
   int strip = 0;      // 1: row-streaming kernel (conv_strip.hip), 0: tile kernel
   ConvCfg cfg{};      // tile kernel configuration
-  int nblk = 32, SR = 0;
+  int nblk = 32, SR = 0, mpi = 128;
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
 };
 
@@ -435,24 +435,27 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
   a.CA = Cin; a.CB = 0; a.RCA = RC; a.RCB = 0; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.upsample = up ? 1 : 0;
   a.Hi = up ? Ho / 2 : (s2 ? Ho * 2 : Ho); a.Wi = up ? Wo / 2 : (s2 ? Wo * 2 : Wo);
-  const int TRs = Wo > 0 ? 128 / Wo : 0;
-  if (!s2 && (Wo == 128 || Wo == 64) && Ho % TRs == 0) {
+  if (!s2 && (Wo == 128 || Wo == 64)) {
     const int nbs[2] = {(Cout % 64 == 0) ? 64 : 32, 32};
-    for (int ni = 0; ni < 2; ++ni) {
-      const int nb = nbs[ni];
-      if (conv_strip_lds_bytes(dt, nb, a) > 160 * 1024) continue;
-      const int nz = (Cout + nb - 1) / nb;
-      int SR = 0;
-      for (int m = 32; m >= 2; m /= 2) {   // longest strip that still gives >= 256 blocks
-        const int sr = TRs * m;
-        if (Ho % sr) continue;
-        SR = sr;
-        if ((Ho / sr) * B * nz >= 256) break;
+    for (int mpi : {256, 128}) {
+      const int TRs = mpi / Wo;
+      if (Ho % TRs) continue;
+      for (int ni = 0; ni < 2; ++ni) {
+        const int nb = nbs[ni];
+        if (conv_strip_lds_bytes(dt, nb, mpi, a) > 160 * 1024) continue;
+        const int nz = (Cout + nb - 1) / nb;
+        int SR = 0;
+        for (int m = 32; m >= 2; m /= 2) {   // longest strip that still gives >= 256 blocks
+          const int sr = TRs * m;
+          if (Ho % sr) continue;
+          SR = sr;
+          if ((Ho / sr) * B * nz >= 256) break;
+        }
+        if (SR == 0) continue;
+        ch.strip = 1; ch.nblk = nb; ch.SR = SR; ch.mpi = mpi;
+        ch.TR = SR; ch.TW = Wo; ch.tiles_x = 1; ch.n_tiles = Ho / SR;
+        return true;
       }
-      if (SR == 0) break;
-      ch.strip = 1; ch.nblk = nb; ch.SR = SR;
-      ch.TR = SR; ch.TW = Wo; ch.tiles_x = 1; ch.n_tiles = Ho / SR;
-      return true;
     }
   }
   ch.strip = 0;
@@ -650,7 +653,7 @@ static int build_plan(sddm_ctx* c, int B) {
                             x.temb_per_b = ctx->rs.temb_per_b;
                             x.t_dev = ctx->rs.t_dev;
                           }
-                          if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.SR, x, B, s);
+                          if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
                           return launch_conv3x3(dt, cfg, x, B, s);
                         }, st.w + (ch.strip ? "[strip]" : "")});
     } else {
