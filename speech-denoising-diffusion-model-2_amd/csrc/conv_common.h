@@ -140,6 +140,92 @@ __device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA
 }  // namespace sddm
 
 namespace sddm {
+// Phase timestamps (profiling builds with -DSDDM_STAMPS only): slot 0 / 7 = s_memrealtime (100 MHz)
+// at block start / end, slots 1..6 = s_memtime (shader clock) at the kernel's phase boundaries.
+#ifdef SDDM_STAMPS
+#define SDDM_STAMP(args, k)                                                                       \
+  do {                                                                                            \
+    if ((args).stamps && threadIdx.x == 0) {                                                      \
+      const size_t blk_ = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z); \
+      (args).stamps[blk_ * 8 + (k)] = ((k) == 0 || (k) == 7) ? __builtin_amdgcn_s_memrealtime()    \
+                                                             : __builtin_amdgcn_s_memtime();      \
+    }                                                                                             \
+  } while (0)
+#else
+#define SDDM_STAMP(args, k) do {} while (0)
+#endif
+
+// floor(n / d) for 0 <= n < 2^21 from the float reciprocal rd = 1 / d: ((n + .5) * rd) is off by
+// less than the .5 / d margin, so the truncation is exact (no integer division sequence).
+__device__ __forceinline__ int fdivi(int n, float rd) { return (int)(((float)n + 0.5f) * rd); }
+
+// GroupNorm statistics of one group loaded in a single round trip (issue() before anything waits,
+// finish() after): up to GK (sum, M2) items per thread; larger producers fall back to the
+// two-pass loop of gn_fused_prologue.  Same fp64 Chan combination in a fixed order.
+struct GNLoad {
+  static constexpr int GK = 12;
+  float2 v[GK];
+  int items, tpg, sub, grp, ntile;
+  bool fast;
+
+  __device__ __forceinline__ void issue(const GNFuse& f, int b, int CA, int CB) {
+    const int C = CA + CB, cpg = C / f.G;
+    tpg = blockDim.x / f.G;
+    grp = threadIdx.x / tpg;
+    sub = threadIdx.x - grp * tpg;
+    const int c0 = grp * cpg;
+    const bool fromA = c0 < CA;
+    const float* st = fromA ? f.statsA : f.statsB;
+    const int tiles = fromA ? f.tilesA : f.tilesB;
+    ntile = fromA ? f.ntileA : f.ntileB;
+    const int Cs = fromA ? CA : CB;
+    const int cs0 = fromA ? c0 : c0 - CA;
+    items = cpg * tiles;
+    fast = items <= GK * tpg;
+    const float* base = st + (size_t)b * tiles * Cs * 2;
+    const float rt = 1.0f / (float)tiles;
+#pragma unroll
+    for (int k = 0; k < GK; ++k) {
+      const int i = sub + k * tpg;
+      v[k] = make_float2(0.f, 0.f);
+      if (fast && grp < f.G && i < items) {
+        const int c = fdivi(i, rt), t = i - c * tiles;
+        v[k] = *(const float2*)(base + ((size_t)t * Cs + cs0 + c) * 2);
+      }
+    }
+  }
+
+  __device__ __forceinline__ void finish(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
+    if (!fast) {
+      gn_fused_prologue(f, b, CA, CB, sc, sh);
+      return;
+    }
+    if (grp >= f.G) return;
+    const int cpg = (CA + CB) / f.G, c0 = grp * cpg;
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < GK; ++k) s += (double)v[k].x;
+    for (int o = 1; o < tpg; o <<= 1) s += __shfl_xor(s, o);
+    const double n_tot = (double)items * ntile;
+    const double mean = s / n_tot;
+    double m2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < GK; ++k) {
+      if (sub + k * tpg < items) {
+        const double d = (double)v[k].x / ntile - mean;
+        m2 += (double)v[k].y + (double)ntile * d * d;
+      }
+    }
+    for (int o = 1; o < tpg; o <<= 1) m2 += __shfl_xor(m2, o);
+    const double rstd = 1.0 / sqrt(m2 / n_tot + (double)f.eps);
+    for (int c = sub; c < cpg; c += tpg) {
+      const double scale = (double)f.gamma[c0 + c] * rstd;
+      sc[c0 + c] = (float)scale;
+      sh[c0 + c] = (float)((double)f.beta[c0 + c] - mean * scale);
+    }
+  }
+};
+
 // =============================================================================================
 // Per-channel tile statistics from an fp32 LDS tile [npix][ld] (values already rounded to the
 // storage type).  Writes (sum, M2 about the tile mean) for channels [0, nch).

@@ -63,6 +63,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   float* red = gsc + 2 * CIN;                     // [NWV waves][NBLK][3]
 
   const int y0 = strip * SR;
+  SDDM_STAMP(a, 0);
   // ---------------- prologue ----------------
   if (gn) {
     const GNFuse f{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
@@ -107,6 +108,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     *(f32x4*)(ring + ((base + r) % R) * SLOT + q * PL + (x + 1) * 16) = v;
   }
   __syncthreads();
+  SDDM_STAMP(a, 3);
 
   int prow[FP], pcol[FP];
 #pragma unroll
@@ -258,6 +260,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     __syncthreads();
   }
 
+  SDDM_STAMP(a, 4);
   // ---- GroupNorm statistics of the strip: lanes -> waves -> block ----
   if (a.stats) {
     const float nl = (float)(FP * iters);
@@ -296,6 +299,8 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       dst[1] = m2;
     }
   }
+  SDDM_STAMP(a, 6);
+  SDDM_STAMP(a, 7);
 }
 
 template <typename T, int FC, int W, int CIN, int MPI>

@@ -68,10 +68,15 @@ struct ConvArgs {
   const void* res_wgt;        // packed [Cout_pad][RCA+RCB] (T)
   void* out;                  // [B][Ho][Wo][Cout]
   float* stats;               // [B][n_tiles][Cout][2] (sum, M2 about tile mean) or null
+  int ck_batch;               // conv_deep: 32-channel input chunks staged in LDS per round trip
+  unsigned long long* stamps; // SDDM_STAMPS builds only: per-block phase timestamps [blocks][8]
+  int dbg;                    // ablation flags for timing experiments (0 in production): 8 = skip the K loop
 };
-struct ConvCfg { int stride2; int kw; int fp; int nblk; };   // K-split waves, pixel frags per wave
-hipError_t launch_conv3x3(int dtype, const ConvCfg& cfg, const ConvArgs& a, int B, hipStream_t s);
-size_t conv3x3_lds_bytes(int dtype, const ConvCfg& cfg, const ConvArgs& a);
+
+// ---- whole-K-resident tile convolution for the narrow levels (conv_deep.hip) ----
+// mt: output pixels per block (32 / 64 / 128); s2: stride-2 Downsample
+hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B, hipStream_t s);
+size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a);
 
 // ---- row-streaming 3x3 convolution for segment widths 64 / 128 (conv_strip.hip) ----
 hipError_t launch_conv_strip(int dtype, int nblk, int mpi, int SR, const ConvArgs& a, int B, hipStream_t s);

@@ -9,12 +9,14 @@
 //   sddm_transition     GaussianDiffusion.p_transition* (model/diffusion.py:164-223)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdarg>
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <functional>
 #include <map>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -202,6 +204,7 @@ struct Op {
   double bytes, flops;
   std::function<hipError_t(hipStream_t)> run;
   std::string name = "";
+  std::function<hipError_t(hipStream_t, int)> run_dbg = nullptr;   // ablation relaunch (timing experiments)
 };
 struct ProfAcc { double ms = 0; int64_t n = 0; double bytes = 0, flops = 0; };
 
@@ -215,6 +218,25 @@ struct RunState {  // fields patched into the plan's kernel arguments at launch 
   float* eps_out = nullptr;
   uint64_t seed = 0;
   int64_t row_offset = 0;
+};
+
+static constexpr int kStreams = 4;    // concurrent lane streams (GPU_MAX_HW_QUEUES is 4)
+static constexpr int kMaxLanes = 64;  // step counters reserved in the weight arena
+
+struct Lane {                         // one row block of the batch: plan + activations + graph
+  int B = 0, row0 = 0, idx = 0;
+  Arena arena;
+  std::vector<Op> ops;
+  RunState rs;
+  size_t off_temb_fwd = 0, off_cond = 0, off_x = 0;
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  int g_K = 0, g_gen = -1;
+  ~Lane() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    if (graph) (void)hipGraphDestroy(graph);
+    arena.reset();
+  }
 };
 
 struct sddm_ctx {
@@ -236,21 +258,20 @@ struct sddm_ctx {
   std::map<std::string, size_t> woff;  // packed weight offsets
   int SC = 0;
   std::map<std::string, int> temb_off;  // per ResnetBlock offset in the projection vector
-  Arena aarena;      // activations of the current plan
+  // the batch is split into lanes of at most lane_rows rows; each lane has its own plan,
+  // activations and step counter, and the lanes' step graphs are replayed concurrently on
+  // kStreams streams (the deep UNet levels are latency-bound: independent lanes fill the chip)
+  std::vector<std::unique_ptr<Lane>> lanes;
   int plan_B = -1;
-  std::vector<Op> ops;
-  size_t off_temb_fwd = 0, off_nl = 0;
-  RunState rs;
-  size_t off_cond = 0, off_x = 0;   // graph-stable copies of cond / x_t
+  int lane_rows = 16;
   int plan_gen = 0;
-  // graph replay of K steps on a private stream
-  hipStream_t work = nullptr;
-  hipEvent_t ev_in = nullptr, ev_out = nullptr;
-  hipGraphExec_t gexec = nullptr;
-  hipGraph_t graph = nullptr;
-  int g_K = 0, g_gen = -1;
+  hipStream_t work[kStreams] = {};
+  hipEvent_t ev_in = nullptr;
+  hipEvent_t ev_done[kStreams] = {};
   bool use_graphs = true;
   // profiling
+  unsigned long long* stamp_buf = nullptr;   // SDDM_STAMPS builds: phase stamps of one op
+  int64_t stamp_blocks = 0;
   bool prof = false;
   std::vector<hipEvent_t> ev_pool;
   std::vector<std::pair<int, int>> ev_used;  // (op cls, pool index of start event)
@@ -372,7 +393,7 @@ static int upload_weights(sddm_ctx* c) {
   }
   c->SC = sc;
   c->off_tables = A.reserve(sizeof(float) * 14 * (c->T + 1));
-  c->off_tdev = A.reserve(64);
+  c->off_tdev = A.reserve(64 * kMaxLanes);
   c->off_temb_tab = A.reserve(sizeof(float) * (size_t)(c->T + 1) * sc);
   SDDM_HIP_CHECK(A.commit());
   for (const auto& b : blobs) SDDM_HIP_CHECK(hipMemcpy(A.base + b.off, b.bytes.data(), b.bytes.size(), hipMemcpyHostToDevice));
@@ -392,42 +413,47 @@ static int upload_tables(sddm_ctx* c) {
 // ---------------------------------------------------------------------------------------------
 // plan: the launch sequence of one UNetModified2 step for batch B
 // ---------------------------------------------------------------------------------------------
-// Tile-kernel configuration: waves split K (kw) when the M x N grid alone cannot fill the chip.
-static int choose_conv_cfg(int dt, int B, ConvArgs& a, ConvCfg& cfg, bool s2) {
-  const int pix = a.Ho * a.Wo;
-  const int nz = (a.Cout + 31) / 32;
-  const int nall = (a.CA + a.CB) / 32 + (a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0);
-  struct Cand { int kw, fp; };
-  std::vector<Cand> cands;
-  const int tiles128 = std::max(1, pix / 128);
-  if (tiles128 * B * nz >= 512 || nall < 2) { cands = {{1, 2}, {1, 1}, {2, 2}}; }
-  else if (nall < 4) { cands = {{2, 4}, {2, 2}, {1, 2}, {1, 1}}; }
-  else { cands = {{4, 8}, {4, 4}, {4, 2}, {2, 4}, {2, 2}, {1, 2}, {1, 1}}; }
-  for (const Cand& cd : cands) {
-    const int mblk = (4 / cd.kw) * cd.fp * 16;
-    if (cd.kw == 4 && mblk > 32 && pix < mblk / 2 * 1) {}  // keep: small images use the smaller tiles below
-    cfg.stride2 = s2 ? 1 : 0;
-    cfg.kw = cd.kw; cfg.fp = cd.fp; cfg.nblk = 32;
-    a.TW = std::min(a.Wo, mblk);
-    a.TR = std::min(mblk / a.TW, a.Ho);
-    if (a.TW * a.TR < mblk && cd.fp > 1 && pix < mblk) continue;   // image smaller than the tile: shrink
-    a.tiles_x = a.Wo / a.TW;
-    a.n_tiles = a.tiles_x * (a.Ho / a.TR);
-    if (conv3x3_lds_bytes(dt, cfg, a) <= 160 * 1024) return 0;
-  }
-  // last resort: smallest tile that fits
-  cfg.kw = 1; cfg.fp = 1; cfg.nblk = 32; cfg.stride2 = s2 ? 1 : 0;
-  a.TW = std::min(a.Wo, 64); a.TR = std::min(64 / a.TW, a.Ho);
-  a.tiles_x = a.Wo / a.TW; a.n_tiles = a.tiles_x * (a.Ho / a.TR);
-  return conv3x3_lds_bytes(dt, cfg, a) <= 160 * 1024 ? 0 : 1;
-}
-
 struct ConvChoice {
-  int strip = 0;      // 1: row-streaming kernel (conv_strip.hip), 0: tile kernel
-  ConvCfg cfg{};      // tile kernel configuration
+  int strip = 0;      // 1: row-streaming kernel (conv_strip.hip), 0: whole-K tile kernel (conv_deep.hip)
   int nblk = 32, SR = 0, mpi = 128;
+  int mt = 0, ckb = 0;                            // conv_deep: pixels per block, chunks per round trip
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
 };
+
+// conv_deep tile: the largest pixel tile (fewest weight re-reads from L2) whose grid still fills
+// the 256 CUs with the whole K resident in LDS; otherwise the tile giving the most blocks.
+static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch) {
+  const int nck = (a.CA + a.CB) / 32, nz = a.Cout / 32;
+  struct Cand { int mt, TR, TW, tiles_x, n_tiles, blocks, ckb; };
+  std::vector<Cand> cs;
+  for (int mt : {128, 64, 32}) {
+    const int TW = std::min(a.Wo, mt);
+    if (mt % TW || a.Wo % TW) continue;
+    const int TR = std::min(mt / TW, a.Ho);
+    if (a.Ho % TR) continue;
+    if (TR * TW < mt && mt > 32) continue;        // partial tiles only at the smallest size
+    a.TR = TR; a.TW = TW; a.tiles_x = a.Wo / TW; a.n_tiles = a.tiles_x * (a.Ho / TR);
+    int ckb = nck;
+    for (; ckb >= 1; --ckb) {
+      a.ck_batch = ckb;
+      if (conv_deep_lds_bytes(dt, mt, s2, a) <= 160 * 1024) break;
+    }
+    if (ckb < 1) continue;
+    cs.push_back({mt, TR, TW, a.tiles_x, a.n_tiles, a.n_tiles * B * nz, ckb});
+  }
+  if (cs.empty()) return false;
+  const Cand* pick = nullptr;
+  for (const Cand& c : cs)
+    if (c.blocks >= 256 && c.ckb == nck) { pick = &c; break; }
+  if (!pick) {
+    pick = &cs[0];
+    for (const Cand& c : cs)
+      if (c.blocks > pick->blocks || (c.blocks == pick->blocks && c.ckb > pick->ckb)) pick = &c;
+  }
+  ch.strip = 0; ch.mt = pick->mt; ch.ckb = pick->ckb;
+  ch.TR = pick->TR; ch.TW = pick->TW; ch.tiles_x = pick->tiles_x; ch.n_tiles = pick->n_tiles;
+  return true;
+}
 
 static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
                         ConvChoice& ch) {
@@ -435,9 +461,13 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
   a.CA = Cin; a.CB = 0; a.RCA = RC; a.RCB = 0; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.upsample = up ? 1 : 0;
   a.Hi = up ? Ho / 2 : (s2 ? Ho * 2 : Ho); a.Wi = up ? Wo / 2 : (s2 ? Wo * 2 : Wo);
-  if (!s2 && (Wo == 128 || Wo == 64)) {
+  // tuning knobs for experiments (unset = defaults): SDDM_STRIP_MPI=128|256, SDDM_STRIP_BLOCKS=target grid
+  static const int env_mpi = std::getenv("SDDM_STRIP_MPI") ? std::atoi(std::getenv("SDDM_STRIP_MPI")) : 0;
+  static const int env_blocks = std::getenv("SDDM_STRIP_BLOCKS") ? std::atoi(std::getenv("SDDM_STRIP_BLOCKS")) : 0;
+  if (!s2 && (Wo == 128 || Wo == 64) && std::getenv("SDDM_NO_STRIP") == nullptr) {
     const int nbs[2] = {(Cout % 64 == 0) ? 64 : 32, 32};
     for (int mpi : {256, 128}) {
+      if (env_mpi && mpi != env_mpi) continue;
       const int TRs = mpi / Wo;
       if (Ho % TRs) continue;
       for (int ni = 0; ni < 2; ++ni) {
@@ -445,11 +475,12 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
         if (conv_strip_lds_bytes(dt, nb, mpi, a) > 160 * 1024) continue;
         const int nz = (Cout + nb - 1) / nb;
         int SR = 0;
-        for (int m = 32; m >= 2; m /= 2) {   // longest strip that still gives >= 256 blocks
+        const int target = env_blocks ? env_blocks : 256;
+        for (int m = 32; m >= 2; m /= 2) {   // longest strip that still gives >= target blocks
           const int sr = TRs * m;
           if (Ho % sr) continue;
           SR = sr;
-          if ((Ho / sr) * B * nz >= 256) break;
+          if ((Ho / sr) * B * nz >= target) break;
         }
         if (SR == 0) continue;
         ch.strip = 1; ch.nblk = nb; ch.SR = SR; ch.mpi = mpi;
@@ -458,22 +489,20 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
       }
     }
   }
-  ch.strip = 0;
-  if (choose_conv_cfg(dt, B, a, ch.cfg, s2)) return false;
-  ch.TR = a.TR; ch.TW = a.TW; ch.tiles_x = a.tiles_x; ch.n_tiles = a.n_tiles;
-  return true;
+  return choose_deep(dt, B, a, s2, ch);
 }
 
-static int build_plan(sddm_ctx* c, int B) {
+static int build_lane(sddm_ctx* c, Lane& L) {
+  const int B = L.B;
+  Lane* lp = &L;
   const int dt = c->dtype;
   const size_t es = dtype_size(dt);
   const UNetCfg& u = c->ucfg;
   const int N = c->num_samples, W = u.seg, S = u.stride;
   const int F = (N - W) / S + 1;
-  c->ops.clear();
-  c->aarena.reset();
-  c->plan_B = -1;
-  Arena& A = c->aarena;
+  L.ops.clear();
+  L.arena.reset();
+  Arena& A = L.arena;
 
   // ---- pass 1: symbolic program + buffer reservations ----
   struct TRes { size_t p, st; int C, H, W, tiles, n_tile; };
@@ -492,10 +521,9 @@ static int build_plan(sddm_ctx* c, int B) {
     gres.push_back({xa, xb, w});
     return (int)gres.size() - 1;
   };
-  c->off_temb_fwd = A.reserve(sizeof(float) * (size_t)B * std::max(c->SC, 1));
-  c->off_cond = A.reserve(sizeof(float) * (size_t)B * N);
-  c->off_x = A.reserve(sizeof(float) * (size_t)B * N);
-  c->off_nl = A.reserve(sizeof(float) * B);
+  L.off_temb_fwd = A.reserve(sizeof(float) * (size_t)B * std::max(c->SC, 1));
+  L.off_cond = A.reserve(sizeof(float) * (size_t)B * N);
+  L.off_x = A.reserve(sizeof(float) * (size_t)B * N);
 
   enum { ST_CONVIN, ST_GN, ST_CONV, ST_FINAL };
   struct Step {
@@ -600,9 +628,9 @@ static int build_plan(sddm_ctx* c, int B) {
       a.out = o.p; a.stats = o.stats; a.TR = TRin;
       const double bytes = (double)B * N * 4 * 2 + (double)B * F * W * u.inner * es;
       const double flops = 2.0 * B * F * W * u.inner * 18;
-      c->ops.push_back({0, bytes, flops, [ctx, a, dt, B](hipStream_t s) {
+      L.ops.push_back({0, bytes, flops, [lp, a, dt, B](hipStream_t s) {
                           ConvInArgs x = a;
-                          x.cond = ctx->rs.cond; x.x = ctx->rs.x; x.t_dev = ctx->rs.t_dev;
+                          x.cond = lp->rs.cond; x.x = lp->rs.x; x.t_dev = lp->rs.t_dev;
                           return launch_conv_in(dt, x, B, s);
                         }, "downs.0"});
     } else if (st.type == ST_CONV) {
@@ -639,23 +667,51 @@ static int build_plan(sddm_ctx* c, int B) {
         flops += 2.0 * B * a.Ho * a.Wo * a.Cout * (double)(ra.C + rb.C);
       }
       const ConvChoice ch = st.ch;
-      const ConvCfg cfg = ch.cfg;
+      const bool s2 = st.s2 != 0;
       a.TR = ch.TR; a.TW = ch.TW; a.tiles_x = ch.tiles_x; a.n_tiles = ch.n_tiles;
       if (a.n_tiles != o.tiles || a.TR * a.TW != o.n_tile) FAIL(SDDM_ERR_STATE, "tile mismatch for %s", st.w.c_str());
       if (Cin % 32 || a.Cout % 32) FAIL(SDDM_ERR_SHAPE, "%s: channels must be multiples of 32", st.w.c_str());
       const bool temb = st.temb;
       const int toff = temb ? c->temb_off.at(st.rb) : 0;
-      c->ops.push_back({2, bytes, flops, [ctx, a, cfg, ch, dt, B, temb, toff](hipStream_t s) {
+#ifdef SDDM_STAMPS
+      if (const char* sn = std::getenv("SDDM_STAMPS")) {
+        if (st.w == sn) {
+          if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
+          SDDM_HIP_CHECK(hipMemset(c->stamp_buf, 0, sizeof(unsigned long long) * 8 * 65536));
+          a.stamps = c->stamp_buf;
+          c->stamp_blocks = ch.strip ? (int64_t)(a.Ho / ch.SR) * B * ((a.Cout + ch.nblk - 1) / ch.nblk)
+                                     : (int64_t)a.n_tiles * B * (a.Cout / 32);
+        }
+      }
+#endif
+      L.ops.push_back({2, bytes, flops, [ctx, lp, a, s2, ch, dt, B, temb, toff](hipStream_t s) {
                           ConvArgs x = a;
                           if (temb) {
-                            x.temb = ctx->rs.temb + toff;
+                            x.temb = lp->rs.temb + toff;
                             x.temb_ld = ctx->SC;
-                            x.temb_per_b = ctx->rs.temb_per_b;
-                            x.t_dev = ctx->rs.t_dev;
+                            x.temb_per_b = lp->rs.temb_per_b;
+                            x.t_dev = lp->rs.t_dev;
                           }
                           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
-                          return launch_conv3x3(dt, cfg, x, B, s);
+                          x.ck_batch = ch.ckb;
+                          return launch_conv_deep(dt, ch.mt, s2, x, B, s);
                         }, st.w + (ch.strip ? "[strip]" : "")});
+      {  // flags: 1 no stats, 2 no GroupNorm transform, 4 no residual / embedding, 8 skip the K loop
+        auto base = L.ops.back().run;
+        ConvArgs a0 = a;
+        L.ops.back().run_dbg = [lp, ctx, a0, s2, ch, dt, B, temb, toff](hipStream_t s, int fl) {
+          ConvArgs x = a0;
+          if (temb && !(fl & 4)) { x.temb = lp->rs.temb + toff; x.temb_ld = ctx->SC; x.temb_per_b = lp->rs.temb_per_b; x.t_dev = lp->rs.t_dev; }
+          if (fl & 1) x.stats = nullptr;
+          if (fl & 2) x.gamma = nullptr;
+          if (fl & 4) x.res_mode = 0;
+          x.dbg = fl;
+          if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
+          x.ck_batch = ch.ckb;
+          return launch_conv_deep(dt, ch.mt, s2, x, B, s);
+        };
+        (void)base;
+      }
     } else {
       FinalArgs f{};
       const Tensor src = TT(st.srcA);
@@ -674,15 +730,35 @@ static int build_plan(sddm_ctx* c, int B) {
       f.co = c->coef();
       const double bytes = (double)B * F * W * src.C * es + (double)B * N * 4 * 3;
       const double flops = 2.0 * B * F * W * src.C * 9;
-      c->ops.push_back({3, bytes, flops, [ctx, f, dt, B](hipStream_t s) {
+      L.ops.push_back({3, bytes, flops, [lp, f, dt, B](hipStream_t s) {
                           FinalArgs x = f;
-                          x.mode = ctx->rs.final_mode; x.eps_out = ctx->rs.eps_out;
-                          x.x = ctx->rs.x; x.cond = ctx->rs.cond; x.t_dev = ctx->rs.t_dev;
-                          x.seed = ctx->rs.seed; x.row_offset = ctx->rs.row_offset;
-                          x.sp = ctx->rs.t_dev ? (const StepParams*)ctx->rs.t_dev : nullptr;
+                          x.mode = lp->rs.final_mode; x.eps_out = lp->rs.eps_out;
+                          x.x = lp->rs.x; x.cond = lp->rs.cond; x.t_dev = lp->rs.t_dev;
+                          x.seed = lp->rs.seed; x.row_offset = lp->rs.row_offset;
+                          x.sp = lp->rs.t_dev ? (const StepParams*)lp->rs.t_dev : nullptr;
                           return launch_final(dt, x, B, s);
                         }, "final_conv"});
     }
+  }
+  return SDDM_OK;
+}
+
+// split the batch into lanes of lane_rows rows (the same per-lane plan for any row partition
+// into multiples of lane_rows, so sharded runs stay bit-identical to a single run)
+static int build_plan(sddm_ctx* c, int B) {
+  c->lanes.clear();
+  c->plan_B = -1;
+  const int LR = std::max(1, c->lane_rows);
+  const int nl = (B + LR - 1) / LR;
+  if (nl > kMaxLanes) FAIL(SDDM_ERR_INVALID_ARG, "batch %d needs %d lanes (max %d): raise SDDM_LANE_ROWS", B, nl, kMaxLanes);
+  for (int l = 0; l < nl; ++l) {
+    std::unique_ptr<Lane> L(new Lane());
+    L->idx = l;
+    L->row0 = l * LR;
+    L->B = std::min(LR, B - l * LR);
+    const int r = build_lane(c, *L);
+    if (r) { c->lanes.clear(); return r; }
+    c->lanes.push_back(std::move(L));
   }
   c->plan_B = B;
   c->plan_gen++;
@@ -709,20 +785,28 @@ static int ensure_ready(sddm_ctx* c) {
   return SDDM_OK;
 }
 
-static int run_ops(sddm_ctx* c, hipStream_t s) {
-  for (const Op& op : c->ops) {
+static int run_ops(sddm_ctx* c, Lane& L, hipStream_t s) {
+  for (const Op& op : L.ops) {
     const bool timed = c->prof && (size_t)(c->ev_used.size() * 2 + 2) <= c->ev_pool.size();
     int e0 = 0;
     if (timed) {
       e0 = (int)c->ev_used.size() * 2;
       SDDM_HIP_CHECK(hipEventRecord(c->ev_pool[e0], s));
     }
-    const hipError_t e = op.run(s);
+    hipError_t e = op.run(s);
     if (e != hipSuccess) FAIL(SDDM_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+    {  // dev knob: SDDM_REPEAT_OP=<layer> SDDM_REPEAT_N=<n> relaunches one (idempotent) layer
+      static const char* rop = std::getenv("SDDM_REPEAT_OP");
+      static const int rn = std::getenv("SDDM_REPEAT_N") ? std::atoi(std::getenv("SDDM_REPEAT_N")) : 0;
+      static const int rflags = std::getenv("SDDM_REPEAT_FLAGS") ? std::atoi(std::getenv("SDDM_REPEAT_FLAGS")) : 0;
+      if (rop && op.name.rfind(rop, 0) == 0)
+        for (int k = 0; k < rn && e == hipSuccess; ++k) e = (rflags && op.run_dbg) ? op.run_dbg(s, rflags) : op.run(s);
+      if (e != hipSuccess) FAIL(SDDM_ERR_HIP, "kernel launch failed: %s", hipGetErrorString(e));
+    }
     if (timed) {
       SDDM_HIP_CHECK(hipEventRecord(c->ev_pool[e0 + 1], s));
       c->ev_used.push_back({op.cls, e0});
-      c->ev_op.push_back((int)(&op - c->ops.data()));
+      c->ev_op.push_back((int)(&op - L.ops.data()));
       c->ev_bytes.push_back(op.bytes);
       c->ev_flops.push_back(op.flops);
     }
@@ -745,6 +829,7 @@ int sddm_create(int device, int compute_dtype, sddm_ctx** out) {
   c->device = device;
   c->dtype = compute_dtype;
   c->use_graphs = std::getenv("SDDM_NO_GRAPH") == nullptr;
+  if (const char* lr = std::getenv("SDDM_LANE_ROWS")) c->lane_rows = std::max(1, std::atoi(lr));
   *out = c;
   return SDDM_OK;
 }
@@ -752,13 +837,13 @@ int sddm_create(int device, int compute_dtype, sddm_ctx** out) {
 void sddm_destroy(sddm_ctx* c) {
   if (!c) return;
   (void)hipSetDevice(c->device);
-  if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
-  if (c->graph) (void)hipGraphDestroy(c->graph);
-  if (c->work) { (void)hipStreamSynchronize(c->work); (void)hipStreamDestroy(c->work); }
+  for (int k = 0; k < kStreams; ++k) {
+    if (c->work[k]) { (void)hipStreamSynchronize(c->work[k]); (void)hipStreamDestroy(c->work[k]); }
+    if (c->ev_done[k]) (void)hipEventDestroy(c->ev_done[k]);
+  }
+  c->lanes.clear();
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
-  if (c->ev_out) (void)hipEventDestroy(c->ev_out);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
-  c->aarena.reset();
   c->warena.reset();
   delete c;
 }
@@ -818,7 +903,7 @@ int sddm_configure(sddm_ctx* c, const char* json) {
     c->tables_dirty = true;
     c->params.clear();
     c->plan_B = -1;
-    c->aarena.reset();
+    c->lanes.clear();
     c->warena.reset();
     c->configured = true;
     return SDDM_OK;
@@ -857,7 +942,7 @@ int sddm_configure(sddm_ctx* c, const char* json) {
   }
   c->params_dirty = true;
   c->plan_B = -1;
-  c->aarena.reset();
+  c->lanes.clear();
   c->warena.reset();
   c->configured = true;
   return SDDM_OK;
@@ -952,27 +1037,9 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
   if (r) return r;
   hipStream_t user = (hipStream_t)stream;
   const bool graph = c->use_graphs && !c->prof && !record;
-  hipStream_t s = user;
-  if (graph) {
-    if (!c->work) {
-      SDDM_HIP_CHECK(hipStreamCreateWithFlags(&c->work, hipStreamNonBlocking));
-      SDDM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
-      SDDM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
-    }
-    SDDM_HIP_CHECK(hipEventRecord(c->ev_in, user));
-    SDDM_HIP_CHECK(hipStreamWaitEvent(c->work, c->ev_in, 0));
-    s = c->work;
-  }
   const int T = c->T;
-  StepParams* sp = c->warena.at<StepParams>(c->off_tdev);
-  int* t_dev = &sp->t;
+  StepParams* sp0 = c->warena.at<StepParams>(c->off_tdev);
   float* temb_tab = c->warena.at<float>(c->off_temb_tab);
-  float* xb = graph ? c->aarena.at<float>(c->off_x) : out;
-  const float* cb = cond;
-  if (graph) {
-    SDDM_HIP_CHECK(hipMemcpyAsync(c->aarena.at<float>(c->off_cond), cond, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
-    cb = c->aarena.at<float>(c->off_cond);
-  }
   // noise-level embeddings of every t (same for all rows: model.py:108)
   EmbedArgs e{};
   e.table = c->dtab(3); e.time_step_mode = c->noise_time_step; e.R = T + 1; e.dim = c->ucfg.inner;
@@ -981,24 +1048,49 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
   e.w2 = c->warena.at<float>(c->woff.at("mlp.w2")); e.b2 = c->warena.at<float>(c->woff.at("mlp.b2"));
   e.pw = c->warena.at<float>(c->woff.at("proj.w")); e.pb = c->warena.at<float>(c->woff.at("proj.b"));
   e.SC = c->SC; e.out = temb_tab;
-  SDDM_HIP_CHECK(launch_embed(e, s));
-  InitArgs ia{};
-  ia.mode = c->init_mode; ia.cond = cb; ia.out = xb; ia.total = B * N; ia.N = N; ia.T = T;
-  ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset;
-  SDDM_HIP_CHECK(launch_init_state(ia, s));
-  SDDM_HIP_CHECK(launch_set_params(sp, T + 1, seed, row_offset, s));
-  c->rs.cond = cb; c->rs.x = xb; c->rs.temb = temb_tab; c->rs.temb_per_b = 0; c->rs.t_dev = t_dev;
-  c->rs.final_mode = c->tr_mode; c->rs.eps_out = nullptr; c->rs.seed = seed; c->rs.row_offset = row_offset;
+  SDDM_HIP_CHECK(launch_embed(e, user));
+  // per-lane state: x_t (graph-stable copy when replaying graphs), condition rows, step counter
+  for (auto& Lp : c->lanes) {
+    Lane& L = *Lp;
+    const int64_t rows = L.B, off = (int64_t)L.row0 * N;
+    float* xb = graph ? L.arena.at<float>(L.off_x) : out + off;
+    const float* cb = cond + off;
+    if (graph) {
+      SDDM_HIP_CHECK(hipMemcpyAsync(L.arena.at<float>(L.off_cond), cb, sizeof(float) * rows * N,
+                                    hipMemcpyDeviceToDevice, user));
+      cb = L.arena.at<float>(L.off_cond);
+    }
+    StepParams* sp = (StepParams*)((char*)sp0 + 64 * L.idx);
+    InitArgs ia{};
+    ia.mode = c->init_mode; ia.cond = cb; ia.out = xb; ia.total = rows * N; ia.N = N; ia.T = T;
+    ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset + L.row0;
+    SDDM_HIP_CHECK(launch_init_state(ia, user));
+    SDDM_HIP_CHECK(launch_set_params(sp, T + 1, seed, row_offset + L.row0, user));
+    L.rs.cond = cb; L.rs.x = xb; L.rs.temb = temb_tab; L.rs.temb_per_b = 0; L.rs.t_dev = &sp->t;
+    L.rs.final_mode = c->tr_mode; L.rs.eps_out = nullptr; L.rs.seed = seed; L.rs.row_offset = row_offset + L.row0;
+  }
   if (graph) {
+    const int ns = std::min<int>(kStreams, (int)c->lanes.size());
+    if (!c->ev_in) SDDM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+    for (int k = 0; k < ns; ++k)
+      if (!c->work[k]) {
+        SDDM_HIP_CHECK(hipStreamCreateWithFlags(&c->work[k], hipStreamNonBlocking));
+        SDDM_HIP_CHECK(hipEventCreateWithFlags(&c->ev_done[k], hipEventDisableTiming));
+      }
+    SDDM_HIP_CHECK(hipEventRecord(c->ev_in, user));
+    for (int k = 0; k < ns; ++k) SDDM_HIP_CHECK(hipStreamWaitEvent(c->work[k], c->ev_in, 0));
     int K = 1;
     for (int k : {10, 8, 5, 4, 2})
       if (T % k == 0) { K = k; break; }
-    if (!c->gexec || c->g_gen != c->plan_gen || c->g_K != K) {
-      if (c->gexec) { (void)hipGraphExecDestroy(c->gexec); c->gexec = nullptr; }
-      if (c->graph) { (void)hipGraphDestroy(c->graph); c->graph = nullptr; }
+    for (auto& Lp : c->lanes) {   // capture K steps of every lane once per plan
+      Lane& L = *Lp;
+      if (L.gexec && L.g_gen == c->plan_gen && L.g_K == K) continue;
+      if (L.gexec) { (void)hipGraphExecDestroy(L.gexec); L.gexec = nullptr; }
+      if (L.graph) { (void)hipGraphDestroy(L.graph); L.graph = nullptr; }
+      hipStream_t s = c->work[L.idx % ns];
       SDDM_HIP_CHECK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
       for (int k = 0; k < K; ++k) {
-        r = run_ops(c, s);
+        r = run_ops(c, L, s);
         if (r) {
           hipGraph_t junk = nullptr;
           (void)hipStreamEndCapture(s, &junk);
@@ -1006,23 +1098,30 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
           return r;
         }
       }
-      SDDM_HIP_CHECK(hipStreamEndCapture(s, &c->graph));
-      SDDM_HIP_CHECK(hipGraphInstantiate(&c->gexec, c->graph, nullptr, nullptr, 0));
-      c->g_gen = c->plan_gen;
-      c->g_K = K;
+      SDDM_HIP_CHECK(hipStreamEndCapture(s, &L.graph));
+      SDDM_HIP_CHECK(hipGraphInstantiate(&L.gexec, L.graph, nullptr, nullptr, 0));
+      L.g_gen = c->plan_gen;
+      L.g_K = K;
     }
-    for (int i = 0; i < T / K; ++i) SDDM_HIP_CHECK(hipGraphLaunch(c->gexec, s));
-    SDDM_HIP_CHECK(hipMemcpyAsync(out, xb, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
-    SDDM_HIP_CHECK(hipEventRecord(c->ev_out, s));
-    SDDM_HIP_CHECK(hipStreamWaitEvent(user, c->ev_out, 0));
+    for (int i = 0; i < T / K; ++i)
+      for (auto& Lp : c->lanes) SDDM_HIP_CHECK(hipGraphLaunch(Lp->gexec, c->work[Lp->idx % ns]));
+    for (auto& Lp : c->lanes)
+      SDDM_HIP_CHECK(hipMemcpyAsync(out + (int64_t)Lp->row0 * N, Lp->rs.x, sizeof(float) * Lp->B * N,
+                                    hipMemcpyDeviceToDevice, c->work[Lp->idx % ns]));
+    for (int k = 0; k < ns; ++k) {
+      SDDM_HIP_CHECK(hipEventRecord(c->ev_done[k], c->work[k]));
+      SDDM_HIP_CHECK(hipStreamWaitEvent(user, c->ev_done[k], 0));
+    }
     return SDDM_OK;
   }
   int64_t nrec = 0;
   for (int t = T; t >= 1; --t) {
-    r = run_ops(c, s);
-    if (r) return r;
+    for (auto& Lp : c->lanes) {
+      r = run_ops(c, *Lp, user);
+      if (r) return r;
+    }
     if (record && t % sample_inter == 0) {  // model.py:100-101: keep x_{t-1} when t % inter == 0
-      SDDM_HIP_CHECK(hipMemcpyAsync(record + nrec * B * N, xb, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));
+      SDDM_HIP_CHECK(hipMemcpyAsync(record + nrec * B * N, out, sizeof(float) * B * N, hipMemcpyDeviceToDevice, user));
       ++nrec;
     }
   }
@@ -1037,18 +1136,24 @@ int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const
   r = prepare_plan(c, B, N);
   if (r) return r;
   hipStream_t s = (hipStream_t)stream;
-  float* temb = c->aarena.at<float>(c->off_temb_fwd);
-  EmbedArgs e{};
-  e.noise_levels = noise_level; e.R = (int)B; e.dim = c->ucfg.inner;
-  e.emb_vec = c->warena.at<float>(c->woff.at("emb_vec"));
-  e.w1 = c->warena.at<float>(c->woff.at("mlp.w1")); e.b1 = c->warena.at<float>(c->woff.at("mlp.b1"));
-  e.w2 = c->warena.at<float>(c->woff.at("mlp.w2")); e.b2 = c->warena.at<float>(c->woff.at("mlp.b2"));
-  e.pw = c->warena.at<float>(c->woff.at("proj.w")); e.pb = c->warena.at<float>(c->woff.at("proj.b"));
-  e.SC = c->SC; e.out = temb;
-  SDDM_HIP_CHECK(launch_embed(e, s));
-  c->rs.cond = cond; c->rs.x = const_cast<float*>(x_t); c->rs.temb = temb; c->rs.temb_per_b = 1;
-  c->rs.t_dev = nullptr; c->rs.final_mode = -1; c->rs.eps_out = eps_out; c->rs.seed = 0; c->rs.row_offset = 0;
-  return run_ops(c, s);
+  for (auto& Lp : c->lanes) {
+    Lane& L = *Lp;
+    const int64_t off = (int64_t)L.row0 * N;
+    float* temb = L.arena.at<float>(L.off_temb_fwd);
+    EmbedArgs e{};
+    e.noise_levels = noise_level + L.row0; e.R = L.B; e.dim = c->ucfg.inner;
+    e.emb_vec = c->warena.at<float>(c->woff.at("emb_vec"));
+    e.w1 = c->warena.at<float>(c->woff.at("mlp.w1")); e.b1 = c->warena.at<float>(c->woff.at("mlp.b1"));
+    e.w2 = c->warena.at<float>(c->woff.at("mlp.w2")); e.b2 = c->warena.at<float>(c->woff.at("mlp.b2"));
+    e.pw = c->warena.at<float>(c->woff.at("proj.w")); e.pb = c->warena.at<float>(c->woff.at("proj.b"));
+    e.SC = c->SC; e.out = temb;
+    SDDM_HIP_CHECK(launch_embed(e, s));
+    L.rs.cond = cond + off; L.rs.x = const_cast<float*>(x_t) + off; L.rs.temb = temb; L.rs.temb_per_b = 1;
+    L.rs.t_dev = nullptr; L.rs.final_mode = -1; L.rs.eps_out = eps_out + off; L.rs.seed = 0; L.rs.row_offset = 0;
+    r = run_ops(c, L, s);
+    if (r) return r;
+  }
+  return SDDM_OK;
 }
 
 int sddm_transition(sddm_ctx* c, int mode, const float* x_t, const float* eps, const float* cond, int t, int64_t B,
@@ -1061,7 +1166,7 @@ int sddm_transition(sddm_ctx* c, int mode, const float* x_t, const float* eps, c
   if (!c->warena.base) {  // tables only (no network needed for a transition)
     c->warena.reset();
     c->off_tables = c->warena.reserve(sizeof(float) * 14 * (c->T + 1));
-    c->off_tdev = c->warena.reserve(64);
+    c->off_tdev = c->warena.reserve(64 * kMaxLanes);
     SDDM_HIP_CHECK(c->warena.commit());
     c->params_dirty = true;
     c->tables_dirty = true;
@@ -1086,7 +1191,7 @@ int sddm_initial_state(sddm_ctx* c, int mode, const float* cond, int64_t B, int6
   if (!c->warena.base) {
     c->warena.reset();
     c->off_tables = c->warena.reserve(sizeof(float) * 14 * (c->T + 1));
-    c->off_tdev = c->warena.reserve(64);
+    c->off_tdev = c->warena.reserve(64 * kMaxLanes);
     SDDM_HIP_CHECK(c->warena.commit());
     c->params_dirty = true;
     c->tables_dirty = true;
@@ -1138,11 +1243,28 @@ int sddm_profile_read(sddm_ctx* c, const char* kernel_class, double* avg_ms, int
   return SDDM_OK;
 }
 
+#ifdef SDDM_STAMPS
+// profiling builds only (not part of the C ABI): copy the phase stamps of the op named by the
+// SDDM_STAMPS environment variable, [blocks][8] u64
+int sddm_debug_stamps(sddm_ctx* c, void* host, int64_t max_blocks, int64_t* n_blocks) {
+  if (!c || !host || !n_blocks) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
+  *n_blocks = 0;
+  if (!c->stamp_buf) return SDDM_OK;
+  const int64_t n = std::min<int64_t>(c->stamp_blocks, max_blocks);
+  SDDM_HIP_CHECK(hipDeviceSynchronize());
+  SDDM_HIP_CHECK(hipMemcpy(host, c->stamp_buf, sizeof(unsigned long long) * 8 * n, hipMemcpyDeviceToHost));
+  *n_blocks = n;
+  return SDDM_OK;
+}
+#endif
+
 int sddm_profile_ops(sddm_ctx* c, char* buf, int64_t buflen) {
   if (!c || !buf || buflen < 3) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
   SDDM_HIP_CHECK(hipSetDevice(c->device));
-  std::vector<double> ms(c->ops.size(), 0.0);
-  std::vector<int64_t> n(c->ops.size(), 0);
+  static const std::vector<Op> kNoOps;
+  const std::vector<Op>& ops = c->lanes.empty() ? kNoOps : c->lanes[0]->ops;   // same layer list in every lane
+  std::vector<double> ms(ops.size(), 0.0);
+  std::vector<int64_t> n(ops.size(), 0);
   for (size_t i = 0; i < c->ev_used.size(); ++i) {
     const int e0 = c->ev_used[i].second, op = c->ev_op[i];
     SDDM_HIP_CHECK(hipEventSynchronize(c->ev_pool[e0 + 1]));
@@ -1152,10 +1274,10 @@ int sddm_profile_ops(sddm_ctx* c, char* buf, int64_t buflen) {
   }
   std::string js = "[";
   char tmp[512];
-  for (size_t i = 0; i < c->ops.size(); ++i) {
+  for (size_t i = 0; i < ops.size(); ++i) {
     snprintf(tmp, sizeof(tmp), "%s{\"name\": \"%s\", \"cls\": %d, \"launches\": %lld, \"avg_ms\": %.6f, \"bytes\": %.0f, \"flops\": %.0f}",
-             i ? ", " : "", c->ops[i].name.c_str(), c->ops[i].cls, (long long)n[i], n[i] ? ms[i] / n[i] : 0.0,
-             c->ops[i].bytes, c->ops[i].flops);
+             i ? ", " : "", ops[i].name.c_str(), ops[i].cls, (long long)n[i], n[i] ? ms[i] / n[i] : 0.0,
+             ops[i].bytes, ops[i].flops);
     js += tmp;
   }
   js += "]";

@@ -10,7 +10,7 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsddm_hip.so")
+LIB_PATH = os.environ.get("SDDM_LIB") or os.path.join(HERE, "libsddm_hip.so")   # SDDM_LIB: profiling variants
 
 OK, ERR_NOT_IMPLEMENTED, ERR_INVALID_ARG, ERR_SHAPE, ERR_HIP, ERR_STATE = range(6)
 F32, BF16, F16 = 0, 1, 2

@@ -16,13 +16,20 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.dirname(HERE)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(os.path.dirname(PKG), "include")
-BUILD = os.path.join(HERE, "_build")
-LIB = os.path.join(HERE, "libsddm_hip.so")
-SOURCES = ["kernels.hip", "conv_strip.hip", "conv_tile.hip", "sddm_runtime.cpp", "schedule.cpp"]
+# SDDM_BUILD_VARIANT=stamps builds a phase-timestamp profiling variant into tools/_stamps/
+VARIANT = os.environ.get("SDDM_BUILD_VARIANT", "")
+if VARIANT:
+    _OUT = os.path.join(os.path.dirname(PKG), "tools", "_" + VARIANT)
+    BUILD = os.path.join(_OUT, "_build")
+    LIB = os.path.join(_OUT, "libsddm_hip.so")
+else:
+    BUILD = os.path.join(HERE, "_build")
+    LIB = os.path.join(HERE, "libsddm_hip.so")
+SOURCES = ["kernels.hip", "conv_strip.hip", "conv_deep.hip", "sddm_runtime.cpp", "schedule.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SDDM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
-         "-Wno-unused-result"]
+         "-Wno-unused-result"] + (["-DSDDM_STAMPS"] if VARIANT == "stamps" else [])
 
 
 def _deps():

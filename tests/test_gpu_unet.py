@@ -59,6 +59,29 @@ def test_unet_forward_reduced_precision(torch_cuda, dtype, tol):
     assert err <= tol
 
 
+@pytest.mark.parametrize("dtype,tol", [("float32", 1e-4), ("bfloat16", 2.5e-2)])
+def test_unet_forward_bench_batch(torch_cuda, dtype, tol):
+    """B=16 x N=16448 (the bench shape): the kernel/tile configurations picked for a full batch
+    (not the B=1 ones) reproduce the reference on every row; rows use mixed noise levels."""
+    N, B = 16448, 16
+    fw = golden("unet_forward.npz")
+    dev = torch_cuda.device("cuda", 0)
+    cond = np.repeat(fw[f"fw/{N}/cond"], B, axis=0)
+    x_t = np.repeat(fw[f"fw/{N}/x_t"], B, axis=0)
+    nl = np.repeat(fw[f"fw/{N}/noise_level"], B, axis=0)
+    ctx = make_ctx(N, dtype)
+    eps = torch_cuda.full((B, 1, N), float("nan"), device=dev)
+    ctx.network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
+                        torch_cuda.from_numpy(nl).to(dev), eps)
+    torch_cuda.cuda.synchronize()
+    eps = eps.cpu().numpy()
+    ref = fw[f"fw/{N}/eps"][0]
+    errs = [rms(eps[b], ref) for b in range(B)]
+    print(f"{dtype} B={B} forward: worst row rms {max(errs):.3e}")
+    assert np.isfinite(eps).all()
+    assert max(errs) <= tol
+
+
 def _sample(torch, ctx, cond_np, seed=7, row_offset=0):
     dev = torch.device("cuda", 0)
     cond = torch.from_numpy(np.ascontiguousarray(cond_np)).to(dev)
