@@ -274,6 +274,25 @@ __device__ __forceinline__ f32x4 transform_fast(f32x4 raw, const float* sc, cons
   return __builtin_bit_cast(f32x4, v);
 }
 
+// GroupNorm affine + SiLU of one 16-byte unit with the per-channel scale / shift read from LDS
+// as 16-byte vectors (sc, sh 16-byte aligned)
+template <typename T>
+__device__ __forceinline__ f32x4 transform_lds(f32x4 raw, const float* sc, const float* sh) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(VE)));
+  float s[VE], h[VE];
+#pragma unroll
+  for (int j = 0; j < VE; j += 4) {
+    const f32x4 a = *(const f32x4*)(sc + j), c = *(const f32x4*)(sh + j);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { s[j + i] = a[i]; h[j + i] = c[i]; }
+  }
+  vec v = __builtin_bit_cast(vec, raw);
+#pragma unroll
+  for (int j = 0; j < VE; ++j) v[j] = from_f32<T>(silu_fast(to_f32<T>(v[j]) * s[j] + h[j]));
+  return __builtin_bit_cast(f32x4, v);
+}
+
 // an MFMA operand fragment whose 16-byte units sit in consecutive planes `stride` bytes apart
 template <typename T> __device__ __forceinline__ Frag<T> load_planes(const char* p, int stride);
 template <> __device__ __forceinline__ Frag<bf16_t> load_planes<bf16_t>(const char* p, int) { return {*(const bf16x8*)p}; }

@@ -40,25 +40,6 @@ __host__ __device__ inline DeepGeo deep_geo(bool s2, int TR, int TW, int MT) {
   return d;
 }
 
-// GroupNorm affine + SiLU of one 16-byte unit with the per-channel scale / shift read from LDS
-// as 16-byte vectors (sc, sh 16-byte aligned)
-template <typename T>
-__device__ __forceinline__ f32x4 transform_lds(f32x4 raw, const float* sc, const float* sh) {
-  constexpr int VE = 16 / (int)sizeof(T);
-  typedef T vec __attribute__((ext_vector_type(VE)));
-  float s[VE], h[VE];
-#pragma unroll
-  for (int j = 0; j < VE; j += 4) {
-    const f32x4 a = *(const f32x4*)(sc + j), c = *(const f32x4*)(sh + j);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { s[j + i] = a[i]; h[j + i] = c[i]; }
-  }
-  vec v = __builtin_bit_cast(vec, raw);
-#pragma unroll
-  for (int j = 0; j < VE; ++j) v[j] = from_f32<T>(silu_fast(to_f32<T>(v[j]) * s[j] + h[j]));
-  return __builtin_bit_cast(f32x4, v);
-}
-
 // Chan merge of (n, mean, M2) partial statistics
 __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
   const float nt = n + nb;
@@ -315,28 +296,46 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
   }
   SDDM_STAMP(a, 5);
   if (a.stats) {
-    // per-thread (n, mean, M2) -> lanes of one channel group (xor 8, 16, 32) -> 4 waves via LDS
-    float mn[4], m2[4], nn[4];
+    // per-thread (n, mean, M2) -> lanes of one channel group (xor 8, 16, 32) -> 4 waves via LDS;
+    // full tiles give every thread the same count, so the merges need no division
+    const bool even = (npv & (PPI - 1)) == 0;
+    float mn[4], m2[4], nn = sn;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      nn[i] = sn;
-      mn[i] = sn > 0.f ? sk[i] + s1[i] / sn : 0.f;
-      m2[i] = sn > 0.f ? fmaxf(s2[i] - s1[i] * s1[i] / sn, 0.f) : 0.f;
+      const float inv = sn > 0.f ? 1.0f / sn : 0.f;
+      mn[i] = sk[i] + s1[i] * inv;
+      m2[i] = fmaxf(s2[i] - s1[i] * s1[i] * inv, 0.f);
     }
+    if (even) {
 #pragma unroll
-    for (int o = 8; o < 64; o <<= 1)
+      for (int o = 8; o < 64; o <<= 1) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float nb = __shfl_xor(nn[i], o), mb = __shfl_xor(mn[i], o), qb = __shfl_xor(m2[i], o);
-        chan_merge(nn[i], mn[i], m2[i], nb, mb, qb);
+        for (int i = 0; i < 4; ++i) {
+          const float mb = __shfl_xor(mn[i], o), qb = __shfl_xor(m2[i], o);
+          const float d = mb - mn[i];
+          m2[i] += qb + d * d * (nn * 0.5f);
+          mn[i] += 0.5f * d;
+        }
+        nn *= 2.f;
       }
+    } else {
+      float nv[4] = {nn, nn, nn, nn};
+#pragma unroll
+      for (int o = 8; o < 64; o <<= 1)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float nb = __shfl_xor(nv[i], o), mb = __shfl_xor(mn[i], o), qb = __shfl_xor(m2[i], o);
+          chan_merge(nv[i], mn[i], m2[i], nb, mb, qb);
+        }
+      nn = nv[0];
+    }
     __syncthreads();                                   // red reads done
     float* xs = red;                                   // [4 waves][8 groups][4 ch][3]
     if (lane < 8)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float* e = xs + ((wave * 8 + lane) * 4 + i) * 3;
-        e[0] = nn[i]; e[1] = mn[i]; e[2] = m2[i];
+        e[0] = nn; e[1] = mn[i]; e[2] = m2[i];
       }
     __syncthreads();
     if (tid < NB) {

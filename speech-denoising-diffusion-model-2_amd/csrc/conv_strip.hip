@@ -43,31 +43,49 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   constexpr int WPLANES = NCK * 9 * 4 * UPL;
   constexpr int PB = 64 / UPP;                    // pixels per 64-unit staging group
   constexpr int NU = TR * W * UPP;                // units of TR rows
-  constexpr int UPT = NU / NT;                    // prefetch units per thread
+  constexpr int UPT = NU / NT;                    // prefetch units per thread and row group
+  constexpr int IU = ((TR + 2) * W * UPP + NT - 1) / NT;   // initial-row units per thread
+  constexpr int RCKM = 4;                         // res_conv chunks held in registers (RC <= 128)
   static_assert(UPP >= 1 && UPP <= 64 && (64 % UPP) == 0, "channel units must divide a wave");
   static_assert(NU % NT == 0, "prefetch must split evenly");
+  typedef T vec4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int strip = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NBLK;
   const int H = a.Ho;
   const int RC = a.RCA + a.RCB;
+  const int rck = a.res_mode == 2 ? RC / 32 : 0;
   const bool gn = a.gamma != nullptr;
-  const bool res2 = a.res_mode == 2;
 
   char* ring = smem;                              // [R][UPP planes][PL]
   char* wl = ring + R * SLOT;                     // [WPLANES][NBLK][16 B]
   char* rw = wl + WPLANES * WPL;                  // [RC*ES/16 planes][NBLK][16 B]
-  const int RPLANES = res2 ? RC * ES / 16 : 0;
+  const int RPLANES = rck * 32 * ES / 16;
   float* gsc = (float*)(rw + RPLANES * WPL);      // [2][CIN]
   float* red = gsc + 2 * CIN;                     // [NWV waves][NBLK][3]
 
   const int y0 = strip * SR;
+  const int iters = SR / TR;
   SDDM_STAMP(a, 0);
-  // ---------------- prologue ----------------
-  if (gn) {
-    const GNFuse f{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-    gn_fused_prologue(f, b, a.CA, a.CB, gsc, gsc + CIN);
+  // ---------------- prologue: every independent load issued before anything waits ----------------
+  GNLoad gl;
+  const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
+  if (gn) gl.issue(gf, b, a.CA, a.CB);
+  // initial ring rows y0-1 .. y0+TR (raw), clamped addresses, zero rows outside the image later
+  const T* srcAb = (const T*)a.srcA + (size_t)b * a.Hi * a.Wi * a.CA;
+  const T* srcBb = a.CB ? (const T*)a.srcB + (size_t)b * a.Hi * a.Wi * a.CB : srcAb;
+  f32x4 ini[IU];
+#pragma unroll
+  for (int k = 0; k < IU; ++k) {
+    const int u = min(tid + k * NT, (TR + 2) * W * UPP - 1);
+    const int grp = u >> 6, j = u & 63;
+    const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
+    const int ry = min(max(y0 - 1 + r, 0), H - 1);
+    const int sy = a.upsample ? ry >> 1 : ry, sx = a.upsample ? x >> 1 : x;
+    const int c0 = q * VE;
+    const bool fa = c0 < a.CA;
+    ini[k] = *(const f32x4*)((fa ? srcAb : srcBb) + ((size_t)sy * a.Wi + sx) * (fa ? a.CA : a.CB) + (fa ? c0 : c0 - a.CA));
   }
   for (int u = tid; u < NBLK * WPLANES; u += NT) {        // co fastest: conflict-free LDS writes
     const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
@@ -75,40 +93,29 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     *(f32x4*)(wl + pl * WPL + co * 16) =
         *(const f32x4*)((const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16);
   }
-  if (res2) {
-    for (int u = tid; u < NBLK * RPLANES; u += NT) {
-      const int co = u % NBLK, pl = u / NBLK;
-      *(f32x4*)(rw + pl * WPL + co * 16) = *(const f32x4*)((const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16);
-    }
+  for (int u = tid; u < NBLK * RPLANES; u += NT) {
+    const int co = u % NBLK, pl = u / NBLK;
+    *(f32x4*)(rw + pl * WPL + co * 16) = *(const f32x4*)((const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16);
   }
   for (int u = tid; u < R * UPP * 2; u += NT) {           // zero halo columns
     const int side = u & 1, pl = u >> 1;
     *(f32x4*)(ring + pl * PL + (side ? (W + 1) : 0) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
   }
+  if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + CIN);
   __syncthreads();                                         // gsc ready
-
-  auto load_unit = [&](int ry, int x, int q) -> f32x4 {
-    if (ry < 0 || ry >= H) return f32x4{0.f, 0.f, 0.f, 0.f};
-    int sy = ry, sx = x;
-    if (a.upsample) { sy >>= 1; sx >>= 1; }
-    const size_t pix = ((size_t)b * a.Hi + sy) * a.Wi + sx;
-    const int c0 = q * VE;
-    if (c0 < a.CA) return *(const f32x4*)((const T*)a.srcA + pix * a.CA + c0);
-    return *(const f32x4*)((const T*)a.srcB + pix * a.CB + (c0 - a.CA));
-  };
   const int base = ((y0 - 1) % R + R) % R;                 // ring slot of row y0 - 1
-
-  // initial rows y0-1 .. y0+TR
-  for (int u = tid; u < (TR + 2) * W * UPP; u += NT) {
+#pragma unroll
+  for (int k = 0; k < IU; ++k) {
+    const int u = tid + k * NT;
+    if (u >= (TR + 2) * W * UPP) break;
     const int grp = u >> 6, j = u & 63;
     const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
     const int ry = y0 - 1 + r;
-    f32x4 v = load_unit(ry, x, q);
-    if (gn && ry >= 0 && ry < H) v = transform_fast<T>(v, gsc + q * VE, gsc + CIN + q * VE);
+    f32x4 v = ini[k];
+    if (ry < 0 || ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
+    else if (gn) v = transform_fast<T>(v, gsc + q * VE, gsc + CIN + q * VE);
     *(f32x4*)(ring + ((base + r) % R) * SLOT + q * PL + (x + 1) * 16) = v;
   }
-  __syncthreads();
-  SDDM_STAMP(a, 3);
 
   int prow[FP], pcol[FP];
 #pragma unroll
@@ -117,31 +124,78 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     prow[fp] = p / W;
     pcol[fp] = p % W;
   }
-  // prefetch geometry of this thread's units (same every iteration): source pointer of row 0
-  // (column and channel offset folded in) and the unit's row inside the TR-row group
-  int pr[UPT], px[UPT], pq[UPT];
-  const char* ubase[UPT];
-  int ustride[UPT];
+  // row-group prefetch geometry of this thread's units (the same every iteration), and the
+  // GroupNorm scale / shift of their channels held in registers
+  int pr[UPT], uoff[UPT], loff[UPT];          // row in group, source offset (elements, +A/B flag), LDS offset
 #pragma unroll
   for (int k = 0; k < UPT; ++k) {
     const int u = tid + k * NT, grp = u >> 6, j = u & 63;
     const int pix = grp * PB + (j % PB);
-    pq[k] = j / PB;
+    const int q = j / PB, x = pix % W;
     pr[k] = pix / W;
-    px[k] = pix % W;
-    const int c0 = pq[k] * VE;
-    const int sx = a.upsample ? (px[k] >> 1) : px[k];
+    loff[k] = q * PL + (x + 1) * 16;
+    const int c0 = q * VE;
+    const int sx = a.upsample ? (x >> 1) : x;
     const bool fa = c0 < a.CA;
-    const int Cs = fa ? a.CA : a.CB;
-    ubase[k] = (const char*)((fa ? (const T*)a.srcA : (const T*)a.srcB) +
-                             (((size_t)b * a.Hi) * a.Wi + sx) * Cs + (fa ? c0 : c0 - a.CA));
-    ustride[k] = a.Wi * Cs * ES;                           // bytes per source row
+    uoff[k] = (fa ? sx * a.CA + c0 : sx * a.CB + (c0 - a.CA)) * 2 + (fa ? 0 : 1);
   }
-  float sK[FC][4], s1[FC][4], s2[FC][4];
+  const int rsA = a.Wi * a.CA, rsB = a.Wi * a.CB;          // elements per source row
+  // rows of row group j (written to the ring at the end of iteration j-1, read by iteration j)
+  auto issue_rows = [&](f32x4 (&dst)[UPT], int j) {
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int ry = min(y0 + j * TR + 1 + pr[k], H - 1);
+      const int sy = a.upsample ? (ry >> 1) : ry;
+      const bool fb = uoff[k] & 1;
+      dst[k] = *(const f32x4*)((fb ? srcBb : srcAb) + (uoff[k] >> 1) + sy * (fb ? rsB : rsA));
+    }
+  };
+  auto commit_rows = [&](const f32x4 (&src)[UPT], int j) {
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int ry = y0 + j * TR + 1 + pr[k];
+      f32x4 v = src[k];
+      if (ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      else if (gn) {
+        const int c0 = (loff[k] / PL) * VE;
+        v = transform_lds<T>(v, gsc + c0, gsc + CIN + c0);
+      }
+      *(f32x4*)(ring + ((base + j * TR + 2 + pr[k]) % R) * SLOT + loff[k]) = v;
+    }
+  };
+  // residual inputs of iteration it (issued one iteration ahead)
+  const T* resb = a.res_mode == 1 ? (const T*)a.res_src + (size_t)b * H * W * a.Cout : nullptr;
+  auto issue_res1 = [&](vec4 (&dst)[FP][FC], int it) {
+#pragma unroll
+    for (int fp = 0; fp < FP; ++fp) {
+      const int yy = min(y0 + it * TR, H - TR) + prow[fp];
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) {
+        const int co = min(n0 + fc * 16 + 4 * g, a.Cout - 4);
+        dst[fp][fc] = *(const vec4*)(resb + ((size_t)yy * W + pcol[fp]) * a.Cout + co);
+      }
+    }
+  };
+  const T* rawAb = rck ? (const T*)a.rawA + (size_t)b * H * W * a.RCA : nullptr;
+  const T* rawBb = (rck && a.RCB) ? (const T*)a.rawB + (size_t)b * H * W * a.RCB : rawAb;
+  auto issue_res2 = [&](Frag<T> (&dst)[RCKM][FP], int it) {
+#pragma unroll
+    for (int ck = 0; ck < RCKM; ++ck)
+#pragma unroll
+      for (int fp = 0; fp < FP; ++fp) {
+        const int yy = min(y0 + it * TR, H - TR) + prow[fp];
+        const int c0 = min(ck, rck - 1) * 32 + g * 8;
+        const size_t pix = (size_t)yy * W + pcol[fp];
+        const T* sp = c0 < a.RCA ? rawAb + pix * a.RCA + c0 : rawBb + pix * a.RCB + (c0 - a.RCA);
+        dst[ck][fp] = load_frag<T>((const char*)sp);
+      }
+  };
+
+  float s1[FC][4], s2[FC][4];                  // sums of (value - badd): shift = bias + embedding
 #pragma unroll
   for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { sK[fc][i] = 0.f; s1[fc][i] = 0.f; s2[fc][i] = 0.f; }
+    for (int i = 0; i < 4; ++i) { s1[fc][i] = 0.f; s2[fc][i] = 0.f; }
   const int t_now = a.t_dev ? *a.t_dev : 0;
   const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : nullptr;
   float badd[FC][4];
@@ -155,22 +209,17 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   const char* abase = wl + g * UPL * WPL + (lane & 15) * 16;
   const char* rbase = rw + g * UPL * WPL + (lane & 15) * 16;
 
-  const int iters = SR / TR;
-  for (int it = 0; it < iters; ++it) {
+  // one iteration: MFMAs on the ring rows of row group it, epilogue, ring refill with row group
+  // it+1 (loaded two iterations earlier); the loads of row group it+3 are issued at the top
+  f32x4 rowsA[UPT], rowsB[UPT], rowsC[UPT];
+  vec4 r1A[FP][FC], r1B[FP][FC];
+  auto body = [&](int it, f32x4 (&nxt)[UPT], f32x4 (&fill)[UPT], vec4 (&r1cur)[FP][FC], vec4 (&r1nxt)[FP][FC]) {
     const int y = y0 + it * TR;
-    const int s_it = (base + it * TR) % R;                 // slot of row y - 1
-    // ---- issue the prefetch of rows y+TR+1 .. y+2TR (raw) ----
-    f32x4 pre[UPT];
-    const bool do_pre = it + 1 < iters;
-    if (do_pre) {
-#pragma unroll
-      for (int k = 0; k < UPT; ++k) {
-        const int ry = y + TR + 1 + pr[k];
-        const int sy = a.upsample ? (ry >> 1) : ry;
-        pre[k] = ry < H ? *(const f32x4*)(ubase[k] + sy * ustride[k]) : f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-    }
-    // ---- MFMA over the 9 taps x CIN/32 chunks of the current rows ----
+    const int s_it = (base + it * TR) % R;               // slot of row y - 1
+    issue_rows(nxt, it + 3);
+    if (a.res_mode == 1) issue_res1(r1nxt, it + 1);
+    Frag<T> r2cur[RCKM][FP];
+    if (rck) issue_res2(r2cur, it);                      // consumed after the 3x3 MFMAs
     f32x4 acc[FP][FC];
 #pragma unroll
     for (int i = 0; i < FP; ++i)
@@ -198,21 +247,15 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         }
       }
     }
-    if (res2) {  // ResnetBlock.res_conv 1x1 on the raw block input, B fragments straight from global
-      for (int ck = 0; ck < RC / 32; ++ck) {
-        Frag<T> bf[FP];
+    if (rck) {  // ResnetBlock.res_conv 1x1 on the raw block input (fragments prefetched)
 #pragma unroll
-        for (int fp = 0; fp < FP; ++fp) {
-          const size_t pix = ((size_t)b * H + y + prow[fp]) * W + pcol[fp];
-          const int c0 = ck * 32 + g * 8;
-          const T* sp = c0 < a.RCA ? (const T*)a.rawA + pix * a.RCA + c0 : (const T*)a.rawB + pix * a.RCB + (c0 - a.RCA);
-          bf[fp] = load_frag<T>((const char*)sp);
-        }
+      for (int ck = 0; ck < RCKM; ++ck) {
+        if (ck >= rck) break;
 #pragma unroll
         for (int fc = 0; fc < FC; ++fc) {
           const Frag<T> af = load_planes<T>(rbase + ck * 4 * UPL * WPL + fc * 256, WPL);
 #pragma unroll
-          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
+          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, r2cur[ck][fp]);
         }
       }
     }
@@ -228,36 +271,36 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = acc[fp][fc][i] + badd[fc][i];
         if (a.res_mode == 1) {
-          const f32x4 r = load4<T>((const T*)a.res_src + po * a.Cout + co);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] += r[i];
+          for (int i = 0; i < 4; ++i) v[i] += (float)r1cur[fp][fc][i];
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = round_t<T>(v[i]);
         store4<T>((T*)a.out + po * a.Cout + co, v[0], v[1], v[2], v[3]);
-        if (it == 0 && fp == 0) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) sK[fc][i] = v[i];
-        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float d = v[i] - sK[fc][i];
+          const float d = v[i] - badd[fc][i];
           s1[fc][i] += d;
           s2[fc][i] += d * d;
         }
       }
     }
-    // ---- transform the prefetched rows into the free ring slots ----
-    if (do_pre) {
-#pragma unroll
-      for (int k = 0; k < UPT; ++k) {
-        const int ry = y + TR + 1 + pr[k];
-        f32x4 v = pre[k];
-        if (gn && ry < H) v = transform_fast<T>(v, gsc + pq[k] * VE, gsc + CIN + pq[k] * VE);
-        *(f32x4*)(ring + ((s_it + TR + 2 + pr[k]) % R) * SLOT + pq[k] * PL + (px[k] + 1) * 16) = v;
-      }
-    }
+    if (it + 1 < iters) commit_rows(fill, it + 1);
     __syncthreads();
+  };
+  if (iters > 1) issue_rows(rowsB, 1);
+  if (iters > 2) issue_rows(rowsC, 2);
+  if (a.res_mode == 1) issue_res1(r1A, 0);
+  __syncthreads();                                         // initial ring rows visible
+  SDDM_STAMP(a, 3);
+  // rotation of the three row-group register sets: group j lives in set j % 3
+  for (int it = 0; it < iters; it += 6) {
+    body(it + 0, rowsA, rowsB, r1A, r1B);
+    if (it + 1 < iters) body(it + 1, rowsB, rowsC, r1B, r1A);
+    if (it + 2 < iters) body(it + 2, rowsC, rowsA, r1A, r1B);
+    if (it + 3 < iters) body(it + 3, rowsA, rowsB, r1B, r1A);
+    if (it + 4 < iters) body(it + 4, rowsB, rowsC, r1A, r1B);
+    if (it + 5 < iters) body(it + 5, rowsC, rowsA, r1B, r1A);
   }
 
   SDDM_STAMP(a, 4);
@@ -269,7 +312,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float n = nl;
-        float mean = sK[fc][i] + s1[fc][i] / nl;
+        float mean = badd[fc][i] + s1[fc][i] / nl;
         float m2 = fmaxf(s2[fc][i] - s1[fc][i] * s1[fc][i] / nl, 0.f);
 #pragma unroll
         for (int o = 1; o < 16; o <<= 1) {   // lanes with the same lane >> 4 hold the same channels

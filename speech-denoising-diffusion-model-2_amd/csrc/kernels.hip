@@ -126,55 +126,105 @@ hipError_t launch_gn_finalize(const GNArgs& a, hipStream_t s) {
 }
 
 // =============================================================================================
-// conv_in: SignalToFrames on cond and x_t (idx[f,w] = S*f + w), channel concat, Conv2d(2, C, 3,
-// pad 1) + bias.  One thread per output pixel, TR frame rows per block.
+// conv_in: SignalToFrames on cond and x_t (idx[f,w] = S*f + w), channel concat, Conv2d(2, 32, 3,
+// pad 1) + bias, as an MFMA over K = 18 taps (2 signals x 3x3, zero-padded to the MFMA depth).
+// T = float: exact f32 MFMA (16x16x4, K = 20); bf16 / f16 storage: fp16 hi/lo split of both
+// operands (x*w = xh*wh + xh*wl + xl*wh, |error| ~ 2^-22 relative) so the fp32 input signal keeps
+// fp32 accuracy.  One block = TR frame rows x W (256 pixels), one wave = 4 fragments of 16 pixels.
 // =============================================================================================
 template <typename T>
 __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   constexpr int CO = 32;                    // inner_channel (checked by the launcher)
   __shared__ float otile[256 * (CO + 1)];   // [pixels][Cout+1] for the tile statistics
   const int b = blockIdx.y, f0 = blockIdx.x * a.TR, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   if (a.t_dev && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.t_dev -= 1;
-  const int npix = a.TR * a.W;
-  const float* cnd = a.cond + (size_t)b * a.N;
-  const float* xx = a.x + (size_t)b * a.N;
-  constexpr int VE = 16 / (int)sizeof(T);
-  typedef T vec __attribute__((ext_vector_type(VE)));
-  for (int p = tid; p < npix; p += blockDim.x) {
-    const int f = f0 + p / a.W, w = p % a.W;
-    float in0[9], in1[9];
+  const float* sig[2] = {a.cond + (size_t)b * a.N, a.x + (size_t)b * a.N};
+  float bias[2][4];
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
+  for (int fc = 0; fc < 2; ++fc)
 #pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const int ff = f + dy - 1, ww = w + dx - 1;
-        const bool ok = ff >= 0 && ff < a.F && ww >= 0 && ww < a.W;
-        const int n = ff * a.S + ww;
-        in0[dy * 3 + dx] = ok ? cnd[n] : 0.f;
-        in1[dy * 3 + dx] = ok ? xx[n] : 0.f;
+    for (int i = 0; i < 4; ++i) bias[fc][i] = a.bias[fc * 16 + 4 * g + i];
+  // this lane's K entries: k -> (signal, dy, dx); sample offset relative to S*f + w
+  constexpr int KPL = sizeof(T) == 4 ? 5 : 8;   // K values per lane per pixel fragment
+  int kch[KPL], kdy[KPL], kdx[KPL];
+  bool kok[KPL];
+#pragma unroll
+  for (int j = 0; j < KPL; ++j) {
+    const int k = sizeof(T) == 4 ? 4 * j + g : 8 * g + j;
+    kok[j] = k < 18;
+    const int kk = kok[j] ? k : 0, ch = kk >= 9 ? 1 : 0, tap = kk - 9 * ch;
+    kch[j] = ch; kdy[j] = tap / 3 - 1; kdx[j] = tap % 3 - 1;
+  }
+  const int F = a.F, W = a.W;
+  // all samples of the wave's 4 fragments are loaded before any is used (clamped addresses)
+  float xs[4][KPL];
+#pragma unroll
+  for (int fr = 0; fr < 4; ++fr) {
+    const int p = wave * 64 + fr * 16 + (lane & 15);
+    const int f = f0 + p / W, w = p % W;
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+      const int ff = f + kdy[j], ww = w + kdx[j];
+      const bool ok = kok[j] && ff >= 0 && ff < F && ww >= 0 && ww < W;
+      xs[fr][j] = (kch[j] ? sig[1] : sig[0])[ok ? ff * a.S + ww : 0];
+      if (!ok) xs[fr][j] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int fr = 0; fr < 4; ++fr) {
+    const int p = wave * 64 + fr * 16 + (lane & 15);
+    const int f = f0 + p / W, w = p % W;
+    f32x4 acc[2];
+    if constexpr (sizeof(T) == 4) {
+      float xb[KPL];
+#pragma unroll
+      for (int j = 0; j < KPL; ++j) xb[j] = xs[fr][j];
+#pragma unroll
+      for (int fc = 0; fc < 2; ++fc) {
+        acc[fc] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const float* wr = a.w + (fc * 16 + (lane & 15)) * 18;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j)
+          acc[fc] = __builtin_amdgcn_mfma_f32_16x16x4f32(kok[j] ? wr[4 * j + g] : 0.f, xb[j], acc[fc], 0, 0, 0);
       }
-    T* op = (T*)a.out + (((size_t)b * a.F + f) * a.W + w) * CO;
-    const float* __restrict__ wg = a.w;      // uniform addresses -> scalar loads, SGPR operands
-    const float* __restrict__ bg = a.bias;
-    for (int c0 = 0; c0 < CO; c0 += VE) {
-      vec v;
+    } else {
+      f16x8 xh, xl;
 #pragma unroll
-      for (int j = 0; j < VE; ++j) {
-        const float* wc = wg + (c0 + j) * 18;
-        float s = 0.f;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) s += wc[k] * in0[k];
-#pragma unroll
-        for (int k = 0; k < 9; ++k) s += wc[9 + k] * in1[k];
-        s += bg[c0 + j];
-        v[j] = from_f32<T>(s);
-        if (p < 256) otile[p * (CO + 1) + c0 + j] = to_f32<T>(v[j]);
+      for (int j = 0; j < KPL; ++j) {
+        const float v = xs[fr][j];
+        xh[j] = (f16_t)v;
+        xl[j] = (f16_t)(v - (float)xh[j]);
       }
-      *(vec*)(op + c0) = v;
+#pragma unroll
+      for (int fc = 0; fc < 2; ++fc) {
+        f16x8 wh, wl;
+        const float* wr = a.w + (fc * 16 + (lane & 15)) * 18;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+          const float v = kok[j] ? wr[8 * g + j] : 0.f;
+          wh[j] = (f16_t)v;
+          wl[j] = (f16_t)(v - (float)wh[j]);
+        }
+        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc[fc], 0, 0, 0);
+        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc[fc], 0, 0, 0);
+      }
+    }
+    T* op = (T*)a.out + (((size_t)b * F + f) * W + w) * CO;
+#pragma unroll
+    for (int fc = 0; fc < 2; ++fc) {
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = round_t<T>(acc[fc][i] + bias[fc][i]);
+        otile[p * (CO + 1) + fc * 16 + 4 * g + i] = v[i];
+      }
+      store4<T>(op + fc * 16 + 4 * g, v[0], v[1], v[2], v[3]);
     }
   }
   __syncthreads();
-  tile_channel_stats(otile, CO + 1, npix, CO, a.stats + ((size_t)b * (a.F / a.TR) + blockIdx.x) * CO * 2, 2);
+  tile_channel_stats(otile, CO + 1, a.TR * W, CO, a.stats + ((size_t)b * (a.F / a.TR) + blockIdx.x) * CO * 2, 2);
 }
 
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s) {
@@ -263,39 +313,78 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   const int PR = YR + 2, PC = W + 2;          // partial-product rows / cols (zero halo cols)
   float* P = (float*)smem;                    // [9][PR][PC]
   float* y = P + 9 * PR * PC;                 // [YR][W]
-  float* wl = y + YR * W;                     // [C][9]
-  float* gs = wl + 9 * C;                     // [2][C]
+  float* gs = y + YR * W;                     // [2][C]
   {
     const GNFuse gf{a.gst, a.gtiles, a.gntile, nullptr, 0, 0, a.gamma, a.beta, a.groups, a.eps};
-    gn_fused_prologue(gf, b, C, 0, gs, gs + C);
+    GNLoad gl;
+    gl.issue(gf, b, C, 0);
+    gl.finish(gf, b, C, 0, gs, gs + C);
   }
-  for (int i = tid; i < 9 * C; i += blockDim.x) wl[i] = a.w[i];   // [c][tap] as Conv2d(C,1,3)
   __syncthreads();
+  // phase 1 as an MFMA: P[tap][pos] = sum_c w[c][tap] * silu(gn(x[c][pos])) with A = the 9 taps
+  // (rows, padded to 16) x 32 channels and B = 32 channels x 16 positions.  bf16 / f16: fp16
+  // hi/lo split of both operands (fp32-accurate products); float: exact f32 MFMA.
+  const int lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const T* src = (const T*)a.src + (size_t)b * F * W * C;
-  const float* __restrict__ wg = a.w;
-  constexpr int VE = 16 / (int)sizeof(T);
-  typedef T vec __attribute__((ext_vector_type(VE)));
-  for (int pp = tid; pp < PR * PC; pp += blockDim.x) {
+  const int tapr = lane & 15;
+  float wv[8], sc[8], sh[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = 8 * g + j;
+    wv[j] = tapr < 9 ? a.w[c * 9 + tapr] : 0.f;
+    sc[j] = gs[c];
+    sh[j] = gs[C + c];
+  }
+  const int npos = PR * PC, nfr = (npos + 15) / 16;
+  // every fragment of this wave is loaded before the first is used (one memory latency, not one
+  // per fragment): FRW fragments per pass
+  constexpr int FRW = 12;
+  typedef T vec8 __attribute__((ext_vector_type(8)));
+  for (int fr0 = wave; fr0 < nfr; fr0 += 4 * FRW) {
+  constexpr int NV = (int)sizeof(T) * 8 / 16;        // 16-byte vectors per 8 channels
+  f32x4 xr[FRW][NV];
+#pragma unroll
+  for (int q = 0; q < FRW; ++q) {
+    const int pp = (fr0 + 4 * q) * 16 + (lane & 15);
     const int r = pp / PC, col = pp - r * PC;
     const int f = f0 - back - 1 + r, w = col - 1;
-    float acc[9];
+    const bool in = pp < npos && f >= 0 && f < F && w >= 0 && w < W;
+    const size_t off = in ? ((size_t)f * W + w) * C + 8 * g : 8 * g;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) acc[k] = 0.f;
-    if (f >= 0 && f < F && w >= 0 && w < W) {
-      const vec* px = (const vec*)(src + ((size_t)f * W + w) * C);
-      for (int q = 0; q < C / VE; ++q) {
-        const vec v = px[q];
+    for (int h = 0; h < NV; ++h) xr[q][h] = *(const f32x4*)((const char*)(src + off) + 16 * h);
+  }
 #pragma unroll
-        for (int j = 0; j < VE; ++j) {
-          const int c = q * VE + j;
-          const float sv = silu(to_f32<T>(v[j]) * gs[c] + gs[C + c]);
+  for (int q = 0; q < FRW; ++q) {
+    const int fr = fr0 + 4 * q;
+    const int pp = fr * 16 + (lane & 15);
+    const int r = pp / PC, col = pp - r * PC;
+    const int f = f0 - back - 1 + r, w = col - 1;
+    const bool in = fr < nfr && pp < npos && f >= 0 && f < F && w >= 0 && w < W;
+    const vec8 x = __builtin_bit_cast(vec8, xr[q]);
+    float v[8];
 #pragma unroll
-          for (int k = 0; k < 9; ++k) acc[k] += wg[c * 9 + k] * sv;   // uniform -> scalar loads
-        }
+    for (int j = 0; j < 8; ++j) v[j] = in ? silu(to_f32<T>(x[j]) * sc[j] + sh[j]) : 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (sizeof(T) == 4) {
+      const Frag<float> A{f32x4{wv[0], wv[1], wv[2], wv[3]}, f32x4{wv[4], wv[5], wv[6], wv[7]}};
+      const Frag<float> Bf{f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}};
+      mfma_frag(acc, A, Bf);
+    } else {
+      f16x8 wh, wl, xh, xl;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        wh[j] = (f16_t)wv[j]; wl[j] = (f16_t)(wv[j] - (float)wh[j]);
+        xh[j] = (f16_t)v[j];  xl[j] = (f16_t)(v[j] - (float)xh[j]);
       }
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
     }
+    if (fr < nfr && pp < npos)
 #pragma unroll
-    for (int k = 0; k < 9; ++k) P[(k * PR + r) * PC + col] = acc[k];
+      for (int i = 0; i < 4; ++i)
+        if (4 * g + i < 9) P[((4 * g + i) * PR + r) * PC + col] = acc[i];
+  }
   }
   __syncthreads();
   for (int p = tid; p < YR * W; p += blockDim.x) {
@@ -342,8 +431,8 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
 
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
   const int back = a.W / a.S - 1, YR = a.FT + back;
-  const size_t lds = ((size_t)9 * (YR + 2) * (a.W + 2) + (size_t)YR * a.W + 9 * a.C + 2 * a.C) * 4;
-  if (lds > 160 * 1024 || a.F % a.FT) return hipErrorInvalidValue;
+  const size_t lds = ((size_t)9 * (YR + 2) * (a.W + 2) + (size_t)YR * a.W + 2 * a.C) * 4;
+  if (lds > 160 * 1024 || a.F % a.FT || a.C != 32) return hipErrorInvalidValue;
   dim3 grid(a.F / a.FT, B);
   if (dtype == DT_F32) hipLaunchKernelGGL(final_kernel<float>, grid, dim3(256), lds, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(final_kernel<bf16_t>, grid, dim3(256), lds, s, a);
