@@ -42,6 +42,7 @@ struct ConvInArgs {
   float* stats;               // [B][tiles][Cout][2]
   int TR;                     // frame rows per block
   int* t_dev;                 // step counter decremented once per launch (may be null)
+  unsigned long long* stamps; // SDDM_STAMPS builds only
 };
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s);
 
@@ -105,6 +106,7 @@ struct FinalArgs {
   TransCoef co;
   uint64_t seed; int64_t row_offset;
   const StepParams* sp;       // when set, seed / row_offset come from device memory (graph replay)
+  unsigned long long* stamps; // SDDM_STAMPS builds only
 };
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s);
 

@@ -12,6 +12,7 @@
 #include "kernels.h"
 #include "conv_common.h"
 #include <algorithm>
+#include <type_traits>
 
 namespace sddm {
 
@@ -128,107 +129,156 @@ hipError_t launch_gn_finalize(const GNArgs& a, hipStream_t s) {
 // =============================================================================================
 // conv_in: SignalToFrames on cond and x_t (idx[f,w] = S*f + w), channel concat, Conv2d(2, 32, 3,
 // pad 1) + bias, as an MFMA over K = 18 taps (2 signals x 3x3, zero-padded to the MFMA depth).
-// T = float: exact f32 MFMA (16x16x4, K = 20); bf16 / f16 storage: fp16 hi/lo split of both
-// operands (x*w = xh*wh + xh*wl + xl*wh, |error| ~ 2^-22 relative) so the fp32 input signal keeps
-// fp32 accuracy.  One block = TR frame rows x W (256 pixels), one wave = 4 fragments of 16 pixels.
+// The block's sample window of both signals is staged in LDS once (two coalesced loads per
+// thread); the framing gathers then read LDS.  T = float: exact f32 MFMA (16x16x4, K = 20);
+// bf16 / f16 storage: fp16 hi/lo split of both operands (x*w = xh*wh + xh*wl + xl*wh, error
+// ~2^-22 relative) so the fp32 signal keeps fp32 accuracy.  A block = TR frame rows x W = 512
+// pixels, a wave = 8 fragments of 16 pixels.  Tile statistics are reduced from registers.
 // =============================================================================================
 template <typename T>
 __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   constexpr int CO = 32;                    // inner_channel (checked by the launcher)
-  __shared__ float otile[256 * (CO + 1)];   // [pixels][Cout+1] for the tile statistics
+  constexpr int IMAX = 6 * 130;             // (TR + 2) x (W + 2) frame image per signal (checked by the launcher)
+  constexpr int NFR = 8;                    // pixel fragments per wave (512 pixels per block)
+  __shared__ float img[2][IMAX];            // zero-bordered frames f0-1 .. f0+TR of cond and x_t
+  __shared__ float xs_red[4][CO][2];        // per-wave channel sums for the tile statistics
   const int b = blockIdx.y, f0 = blockIdx.x * a.TR, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   if (a.t_dev && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.t_dev -= 1;
-  const float* sig[2] = {a.cond + (size_t)b * a.N, a.x + (size_t)b * a.N};
+  SDDM_STAMP(a, 0);
+  const int S = a.S, F = a.F, W = a.W, IW = W + 2, IH = a.TR + 2;
+  {
+    const float* c0 = a.cond + (size_t)b * a.N;
+    const float* x0 = a.x + (size_t)b * a.N;
+    for (int i = tid; i < IH * IW; i += 256) {
+      const int r = i / IW, c = i - r * IW, f = f0 - 1 + r, w = c - 1;
+      const bool ok = f >= 0 && f < F && w >= 0 && w < W;
+      const int n = ok ? f * S + w : 0;
+      img[0][i] = ok ? c0[n] : 0.f;
+      img[1][i] = ok ? x0[n] : 0.f;
+    }
+  }
   float bias[2][4];
 #pragma unroll
   for (int fc = 0; fc < 2; ++fc)
 #pragma unroll
     for (int i = 0; i < 4; ++i) bias[fc][i] = a.bias[fc * 16 + 4 * g + i];
-  // this lane's K entries: k -> (signal, dy, dx); sample offset relative to S*f + w
+  // this lane's K entries k -> (signal, dy, dx) as offsets into the frame image (k >= 18: zero)
   constexpr int KPL = sizeof(T) == 4 ? 5 : 8;   // K values per lane per pixel fragment
-  int kch[KPL], kdy[KPL], kdx[KPL];
+  int koff[KPL];
   bool kok[KPL];
+  float wf[2][KPL];                             // weights as MFMA A operands (rows = output channels)
 #pragma unroll
   for (int j = 0; j < KPL; ++j) {
     const int k = sizeof(T) == 4 ? 4 * j + g : 8 * g + j;
     kok[j] = k < 18;
     const int kk = kok[j] ? k : 0, ch = kk >= 9 ? 1 : 0, tap = kk - 9 * ch;
-    kch[j] = ch; kdy[j] = tap / 3 - 1; kdx[j] = tap % 3 - 1;
+    koff[j] = ch * IMAX + (tap / 3) * IW + (tap % 3);
+#pragma unroll
+    for (int fc = 0; fc < 2; ++fc) wf[fc][j] = kok[j] ? a.w[(fc * 16 + (lane & 15)) * 18 + k] : 0.f;
   }
-  const int F = a.F, W = a.W;
-  // all samples of the wave's 4 fragments are loaded before any is used (clamped addresses)
-  float xs[4][KPL];
+  f16x8 wh[2], wl[2];
 #pragma unroll
-  for (int fr = 0; fr < 4; ++fr) {
-    const int p = wave * 64 + fr * 16 + (lane & 15);
-    const int f = f0 + p / W, w = p % W;
+  for (int fc = 0; fc < 2; ++fc)
 #pragma unroll
-    for (int j = 0; j < KPL; ++j) {
-      const int ff = f + kdy[j], ww = w + kdx[j];
-      const bool ok = kok[j] && ff >= 0 && ff < F && ww >= 0 && ww < W;
-      xs[fr][j] = (kch[j] ? sig[1] : sig[0])[ok ? ff * a.S + ww : 0];
-      if (!ok) xs[fr][j] = 0.f;
+    for (int j = 0; j < 8; ++j) {
+      const float v = j < KPL ? wf[fc][j] : 0.f;
+      wh[fc][j] = (f16_t)v;
+      wl[fc][j] = (f16_t)(v - (float)wh[fc][j]);
     }
-  }
+  float st1[2][4], st2[2][4];
 #pragma unroll
-  for (int fr = 0; fr < 4; ++fr) {
-    const int p = wave * 64 + fr * 16 + (lane & 15);
-    const int f = f0 + p / W, w = p % W;
+  for (int fc = 0; fc < 2; ++fc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { st1[fc][i] = 0.f; st2[fc][i] = 0.f; }
+  __syncthreads();                                        // frame image staged
+  SDDM_STAMP(a, 1);
+  const float* imgf = &img[0][0];
+#pragma unroll 2
+  for (int fr = 0; fr < NFR; ++fr) {
+    const int p = wave * (NFR * 16) + fr * 16 + (lane & 15);
+    const int r = p / W, w = p - r * W;
+    const int pb = r * IW + w;                              // image index of tap (0, 0)
+    float xv[KPL];
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) xv[j] = kok[j] ? imgf[pb + koff[j]] : 0.f;
     f32x4 acc[2];
-    if constexpr (sizeof(T) == 4) {
-      float xb[KPL];
-#pragma unroll
-      for (int j = 0; j < KPL; ++j) xb[j] = xs[fr][j];
+    if constexpr (sizeof(T) == 4) {                          // exact fp32 MFMA
 #pragma unroll
       for (int fc = 0; fc < 2; ++fc) {
         acc[fc] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const float* wr = a.w + (fc * 16 + (lane & 15)) * 18;
 #pragma unroll
-        for (int j = 0; j < KPL; ++j)
-          acc[fc] = __builtin_amdgcn_mfma_f32_16x16x4f32(kok[j] ? wr[4 * j + g] : 0.f, xb[j], acc[fc], 0, 0, 0);
+        for (int j = 0; j < KPL; ++j) acc[fc] = __builtin_amdgcn_mfma_f32_16x16x4f32(wf[fc][j], xv[j], acc[fc], 0, 0, 0);
       }
-    } else {
+    } else if constexpr (std::is_same<T, bf16_t>::value) {  // bf16 storage: fp16 operands (2^-11 << 2^-8)
+      f16x8 xh;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) xh[j] = (f16_t)(j < KPL ? xv[j] : 0.f);
+#pragma unroll
+      for (int fc = 0; fc < 2; ++fc)
+        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[fc], xh, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    } else {                                                  // f16 storage: hi/lo split (fp32-accurate)
       f16x8 xh, xl;
 #pragma unroll
-      for (int j = 0; j < KPL; ++j) {
-        const float v = xs[fr][j];
+      for (int j = 0; j < 8; ++j) {
+        const float v = j < KPL ? xv[j] : 0.f;
         xh[j] = (f16_t)v;
         xl[j] = (f16_t)(v - (float)xh[j]);
       }
 #pragma unroll
       for (int fc = 0; fc < 2; ++fc) {
-        f16x8 wh, wl;
-        const float* wr = a.w + (fc * 16 + (lane & 15)) * 18;
-#pragma unroll
-        for (int j = 0; j < KPL; ++j) {
-          const float v = kok[j] ? wr[8 * g + j] : 0.f;
-          wh[j] = (f16_t)v;
-          wl[j] = (f16_t)(v - (float)wh[j]);
-        }
-        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc[fc], 0, 0, 0);
-        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc[fc], 0, 0, 0);
+        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[fc], xh, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh[fc], xl, acc[fc], 0, 0, 0);
+        acc[fc] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[fc], xh, acc[fc], 0, 0, 0);
       }
     }
-    T* op = (T*)a.out + (((size_t)b * F + f) * W + w) * CO;
+    T* op = (T*)a.out + (((size_t)b * F + f0 + r) * W + w) * CO;
 #pragma unroll
     for (int fc = 0; fc < 2; ++fc) {
       float v[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         v[i] = round_t<T>(acc[fc][i] + bias[fc][i]);
-        otile[p * (CO + 1) + fc * 16 + 4 * g + i] = v[i];
+        const float d = v[i] - bias[fc][i];     // shift = bias (common to the whole tile)
+        st1[fc][i] += d;
+        st2[fc][i] += d * d;
       }
       store4<T>(op + fc * 16 + 4 * g, v[0], v[1], v[2], v[3]);
     }
   }
+  SDDM_STAMP(a, 2);
+  // tile statistics: lanes of one channel group (xor 1..8) -> 4 waves (LDS), plain sums about the bias
+#pragma unroll
+  for (int fc = 0; fc < 2; ++fc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        st1[fc][i] += __shfl_xor(st1[fc][i], o);
+        st2[fc][i] += __shfl_xor(st2[fc][i], o);
+      }
+      if ((lane & 15) == 0) {
+        xs_red[wave][fc * 16 + 4 * g + i][0] = st1[fc][i];
+        xs_red[wave][fc * 16 + 4 * g + i][1] = st2[fc][i];
+      }
+    }
   __syncthreads();
-  tile_channel_stats(otile, CO + 1, a.TR * W, CO, a.stats + ((size_t)b * (a.F / a.TR) + blockIdx.x) * CO * 2, 2);
+  SDDM_STAMP(a, 3);
+  if (tid < CO) {
+    const float n = (float)(a.TR * W);
+    float S1 = 0.f, S2 = 0.f;
+#pragma unroll
+    for (int w4 = 0; w4 < 4; ++w4) { S1 += xs_red[w4][tid][0]; S2 += xs_red[w4][tid][1]; }
+    float* dst = a.stats + (((size_t)b * (a.F / a.TR) + blockIdx.x) * CO + tid) * 2;
+    dst[0] = a.bias[tid] * n + S1;                 // sum
+    dst[1] = fmaxf(S2 - S1 * S1 / n, 0.f);        // M2 about the tile mean
+  }
+  SDDM_STAMP(a, 6);
+  SDDM_STAMP(a, 7);
 }
 
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s) {
-  if (a.Cout != 32 || a.TR * a.W != 256 || a.F % a.TR) return hipErrorInvalidValue;
+  if (a.Cout != 32 || a.TR * a.W != 512 || a.F % a.TR || (a.TR + 2) * (a.W + 2) > 6 * 130) return hipErrorInvalidValue;
   dim3 grid(a.F / a.TR, B);
   if (dtype == DT_F32) hipLaunchKernelGGL(conv_in_kernel<float>, grid, dim3(256), 0, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(conv_in_kernel<bf16_t>, grid, dim3(256), 0, s, a);
@@ -304,7 +354,7 @@ __global__ __launch_bounds__(256) void init_state_kernel(InitArgs a) {
 //           consecutive samples per thread (one Philox counter group).
 // =============================================================================================
 template <typename T>
-__global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
+__global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int b = blockIdx.y, f0 = blockIdx.x * a.FT, tid = threadIdx.x;
   const int C = a.C, W = a.W, S = a.S, F = a.F;
@@ -314,6 +364,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   float* P = (float*)smem;                    // [9][PR][PC]
   float* y = P + 9 * PR * PC;                 // [YR][W]
   float* gs = y + YR * W;                     // [2][C]
+  SDDM_STAMP(a, 0);
   {
     const GNFuse gf{a.gst, a.gtiles, a.gntile, nullptr, 0, 0, a.gamma, a.beta, a.groups, a.eps};
     GNLoad gl;
@@ -321,6 +372,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
     gl.finish(gf, b, C, 0, gs, gs + C);
   }
   __syncthreads();
+  SDDM_STAMP(a, 1);
   // phase 1 as an MFMA: P[tap][pos] = sum_c w[c][tap] * silu(gn(x[c][pos])) with A = the 9 taps
   // (rows, padded to 16) x 32 channels and B = 32 channels x 16 positions.  bf16 / f16: fp16
   // hi/lo split of both operands (fp32-accurate products); float: exact f32 MFMA.
@@ -338,14 +390,14 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   const int npos = PR * PC, nfr = (npos + 15) / 16;
   // every fragment of this wave is loaded before the first is used (one memory latency, not one
   // per fragment): FRW fragments per pass
-  constexpr int FRW = 12;
+  constexpr int NWV = 8, FRW = 12;                   // waves per block, fragments per wave and pass
   typedef T vec8 __attribute__((ext_vector_type(8)));
-  for (int fr0 = wave; fr0 < nfr; fr0 += 4 * FRW) {
+  for (int fr0 = wave; fr0 < nfr; fr0 += NWV * FRW) {
   constexpr int NV = (int)sizeof(T) * 8 / 16;        // 16-byte vectors per 8 channels
   f32x4 xr[FRW][NV];
 #pragma unroll
   for (int q = 0; q < FRW; ++q) {
-    const int pp = (fr0 + 4 * q) * 16 + (lane & 15);
+    const int pp = (fr0 + NWV * q) * 16 + (lane & 15);
     const int r = pp / PC, col = pp - r * PC;
     const int f = f0 - back - 1 + r, w = col - 1;
     const bool in = pp < npos && f >= 0 && f < F && w >= 0 && w < W;
@@ -355,7 +407,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   }
 #pragma unroll
   for (int q = 0; q < FRW; ++q) {
-    const int fr = fr0 + 4 * q;
+    const int fr = fr0 + NWV * q;
     const int pp = fr * 16 + (lane & 15);
     const int r = pp / PC, col = pp - r * PC;
     const int f = f0 - back - 1 + r, w = col - 1;
@@ -363,7 +415,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
     const vec8 x = __builtin_bit_cast(vec8, xr[q]);
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = in ? silu(to_f32<T>(x[j]) * sc[j] + sh[j]) : 0.f;
+    for (int j = 0; j < 8; ++j) v[j] = in ? silu_fast(to_f32<T>(x[j]) * sc[j] + sh[j]) : 0.f;
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if constexpr (sizeof(T) == 4) {
       const Frag<float> A{f32x4{wv[0], wv[1], wv[2], wv[3]}, f32x4{wv[4], wv[5], wv[6], wv[7]}};
@@ -377,8 +429,10 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
         xh[j] = (f16_t)v[j];  xl[j] = (f16_t)(v[j] - (float)xh[j]);
       }
       acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
+      if constexpr (!std::is_same<T, bf16_t>::value) {   // bf16 storage: the fp16 products suffice
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
+      }
     }
     if (fr < nfr && pp < npos)
 #pragma unroll
@@ -387,6 +441,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
   }
   }
   __syncthreads();
+  SDDM_STAMP(a, 2);
   for (int p = tid; p < YR * W; p += blockDim.x) {
     const int r = p / W, w = p - r * W;        // y row r <-> P rows r .. r+2, cols w .. w+2
     float s = 0.f;
@@ -397,6 +452,7 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
     y[p] = s + a.bias;
   }
   __syncthreads();
+  SDDM_STAMP(a, 3);
   const int n_begin = f0 * S;
   const int n_end = (f0 + a.FT >= F) ? a.N : (f0 + a.FT) * S;
   const int t = a.t_dev ? *a.t_dev : 0;
@@ -427,6 +483,8 @@ __global__ __launch_bounds__(256) void final_kernel(FinalArgs a) {
       }
     }
   }
+  SDDM_STAMP(a, 6);
+  SDDM_STAMP(a, 7);
 }
 
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
@@ -434,9 +492,9 @@ hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
   const size_t lds = ((size_t)9 * (YR + 2) * (a.W + 2) + (size_t)YR * a.W + 2 * a.C) * 4;
   if (lds > 160 * 1024 || a.F % a.FT || a.C != 32) return hipErrorInvalidValue;
   dim3 grid(a.F / a.FT, B);
-  if (dtype == DT_F32) hipLaunchKernelGGL(final_kernel<float>, grid, dim3(256), lds, s, a);
-  else if (dtype == DT_BF16) hipLaunchKernelGGL(final_kernel<bf16_t>, grid, dim3(256), lds, s, a);
-  else hipLaunchKernelGGL(final_kernel<f16_t>, grid, dim3(256), lds, s, a);
+  if (dtype == DT_F32) hipLaunchKernelGGL(final_kernel<float>, grid, dim3(512), lds, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(final_kernel<bf16_t>, grid, dim3(512), lds, s, a);
+  else hipLaunchKernelGGL(final_kernel<f16_t>, grid, dim3(512), lds, s, a);
   return hipGetLastError();
 }
 

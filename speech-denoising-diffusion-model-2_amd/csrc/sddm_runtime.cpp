@@ -539,9 +539,9 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   auto pick = [&](int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up, ConvChoice& ch) {
     return choose_conv(dt, B, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch);
   };
-  const int TRin = 256 / W;
-  if (u.inner != 32 || 256 % W || F % TRin)
-    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "conv_in needs inner_channel 32 and segment_len dividing 256 (got %d, %d)", u.inner, W);
+  const int TRin = 512 / W;
+  if (u.inner != 32 || 512 % W || F % TRin || (TRin + 1) * S + W + 2 > 1024)
+    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "conv_in needs inner_channel 32 and segment_len dividing 512 (got %d, %d)", u.inner, W);
   const int t0 = new_tensor(u.inner, F, W, F / TRin, TRin * W);
   { Step st; st.type = ST_CONVIN; st.out = t0; prog.push_back(st); }
 
@@ -628,6 +628,14 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       a.out = o.p; a.stats = o.stats; a.TR = TRin;
       const double bytes = (double)B * N * 4 * 2 + (double)B * F * W * u.inner * es;
       const double flops = 2.0 * B * F * W * u.inner * 18;
+#ifdef SDDM_STAMPS
+      if (const char* sn = std::getenv("SDDM_STAMPS"))
+        if (std::string(sn) == "downs.0") {
+          if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
+          a.stamps = c->stamp_buf;
+          c->stamp_blocks = (int64_t)(F / TRin) * B;
+        }
+#endif
       L.ops.push_back({0, bytes, flops, [lp, a, dt, B](hipStream_t s) {
                           ConvInArgs x = a;
                           x.cond = lp->rs.cond; x.x = lp->rs.x; x.t_dev = lp->rs.t_dev;
@@ -730,6 +738,14 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       f.co = c->coef();
       const double bytes = (double)B * F * W * src.C * es + (double)B * N * 4 * 3;
       const double flops = 2.0 * B * F * W * src.C * 9;
+#ifdef SDDM_STAMPS
+      if (const char* sn = std::getenv("SDDM_STAMPS"))
+        if (std::string(sn) == "final_conv") {
+          if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
+          f.stamps = c->stamp_buf;
+          c->stamp_blocks = (int64_t)(F / f.FT) * B;
+        }
+#endif
       L.ops.push_back({3, bytes, flops, [lp, f, dt, B](hipStream_t s) {
                           FinalArgs x = f;
                           x.mode = lp->rs.final_mode; x.eps_out = lp->rs.eps_out;

@@ -20,6 +20,11 @@ __global__ void k_chase(const int* __restrict__ idx, float* out, int hops, int n
   for (int h = 0; h < hops; ++h) j = idx[j];
   out[(blockIdx.x * blockDim.x + threadIdx.x) % n] = (float)j;
 }
+__global__ void k_spin(float* out, int iters) {
+  float v = threadIdx.x * 1e-3f;
+  for (int i = 0; i < iters; ++i) v = v * 0.999f + 1e-3f;
+  if (v == -1.f) out[0] = v;
+}
 __global__ void k_barriers(float* out, int nb) {
   __shared__ float s[256];
   float v = threadIdx.x;
@@ -87,6 +92,88 @@ int main() {
       printf(" | chase%-2d(16MB) %6.2f", hops, time_graph(s, R, [&] { hipLaunchKernelGGL(k_chase, dim3(blocks), dim3(256), 0, s, idx, out, hops, n); }));
     printf(" | 20 barriers %6.2f", time_graph(s, R, [&] { hipLaunchKernelGGL(k_barriers, dim3(blocks), dim3(256), 0, s, out, 10); }));
     printf(" | 8x(store+barrier) %6.2f\n", time_graph(s, R, [&] { hipLaunchKernelGGL(k_store_then_barrier, dim3(blocks), dim3(256), 0, s, out, n, 8); }));
+  }
+  {  // stream concurrency: two graphs (each R chase kernels of 80 blocks) on one vs two streams
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    auto mk = [&](hipStream_t st, hipGraphExec_t* ge) {
+      hipGraph_t g;
+      (void)hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal);
+      for (int i = 0; i < R; ++i) hipLaunchKernelGGL(k_spin, dim3(80), dim3(256), 0, st, out, 4000);
+      (void)hipStreamEndCapture(st, &g);
+      (void)hipGraphInstantiate(ge, g, nullptr, nullptr, 0);
+    };
+    hipGraphExec_t g1, g2;
+    mk(s, &g1);
+    mk(s2, &g2);
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0); (void)hipEventCreate(&e1);
+    for (int mode = 0; mode < 2; ++mode) {
+      (void)hipDeviceSynchronize();
+      (void)hipEventRecord(e0, s);
+      (void)hipStreamWaitEvent(s2, e0, 0);
+      for (int k = 0; k < 3; ++k) {
+        (void)hipGraphLaunch(g1, s);
+        (void)hipGraphLaunch(g2, mode ? s2 : s);
+      }
+      hipEvent_t e2;
+      (void)hipEventCreate(&e2);
+      (void)hipEventRecord(e2, s2);
+      (void)hipStreamWaitEvent(s, e2, 0);
+      (void)hipEventRecord(e1, s);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      printf("two graphs of %d spin kernels x3 on %s: %.1f us per kernel pair\n", R, mode ? "two streams" : "one stream", ms * 1000.f / (3 * R));
+    }
+  }
+  {  // (a) eager launches alternating on two streams; (b) one graph with two parallel branches
+    hipStream_t s2;
+    CK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    hipEvent_t e0, e1, e2;
+    (void)hipEventCreate(&e0); (void)hipEventCreate(&e1); (void)hipEventCreate(&e2);
+    for (int mode = 0; mode < 2; ++mode) {
+      (void)hipDeviceSynchronize();
+      (void)hipEventRecord(e0, s);
+      (void)hipStreamWaitEvent(s2, e0, 0);
+      for (int i = 0; i < R; ++i) {
+        hipLaunchKernelGGL(k_spin, dim3(80), dim3(256), 0, s, out, 4000);
+        hipLaunchKernelGGL(k_spin, dim3(80), dim3(256), 0, mode ? s2 : s, out, 4000);
+      }
+      (void)hipEventRecord(e2, s2);
+      (void)hipStreamWaitEvent(s, e2, 0);
+      (void)hipEventRecord(e1, s);
+      (void)hipEventSynchronize(e1);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      printf("eager pairs of spin kernels on %s: %.1f us per pair\n", mode ? "two streams" : "one stream", ms * 1000.f / R);
+    }
+    // one graph, two branches forked from s
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    hipEvent_t ef, ej;
+    (void)hipEventCreateWithFlags(&ef, hipEventDisableTiming);
+    (void)hipEventCreateWithFlags(&ej, hipEventDisableTiming);
+    (void)hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal);
+    (void)hipEventRecord(ef, s);
+    (void)hipStreamWaitEvent(s2, ef, 0);
+    for (int i = 0; i < R; ++i) {
+      hipLaunchKernelGGL(k_spin, dim3(80), dim3(256), 0, s, out, 4000);
+      hipLaunchKernelGGL(k_spin, dim3(80), dim3(256), 0, s2, out, 4000);
+    }
+    (void)hipEventRecord(ej, s2);
+    (void)hipStreamWaitEvent(s, ej, 0);
+    (void)hipStreamEndCapture(s, &g);
+    (void)hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    (void)hipGraphLaunch(ge, s);
+    (void)hipStreamSynchronize(s);
+    (void)hipEventRecord(e0, s);
+    for (int k = 0; k < 3; ++k) (void)hipGraphLaunch(ge, s);
+    (void)hipEventRecord(e1, s);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    printf("one graph with two parallel branches: %.1f us per pair\n", ms * 1000.f / (3 * R));
   }
   int lds_kb = 128;
   printf("empty kernel with %d KB dynamic LDS, 256 blocks: %6.2f us\n", lds_kb,
