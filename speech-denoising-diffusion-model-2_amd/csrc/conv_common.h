@@ -161,10 +161,11 @@ __device__ __forceinline__ int fdivi(int n, float rd) { return (int)(((float)n +
 
 // GroupNorm statistics of one group loaded in a single round trip (issue() before anything waits,
 // finish() after): up to GK (sum, M2) items per thread; larger producers fall back to the
-// two-pass loop of gn_fused_prologue.  Same fp64 Chan combination in a fixed order.
+// two-pass loop of gn_fused_prologue (fp64).  Chan combination in a fixed order.
 struct GNLoad {
   static constexpr int GK = 12;
   float2 v[GK];
+  float gm, bt;                 // gamma / beta of channel c0 + sub (sub < cpg), loaded with the items
   int items, tpg, sub, grp, ntile;
   bool fast;
 
@@ -181,18 +182,23 @@ struct GNLoad {
     const int Cs = fromA ? CA : CB;
     const int cs0 = fromA ? c0 : c0 - CA;
     items = cpg * tiles;
-    fast = items <= GK * tpg;
     const float* base = st + (size_t)b * tiles * Cs * 2;
     const float rt = 1.0f / (float)tiles;
+    // GK loads per thread, unconditional at clamped indices (a conditional load makes the
+    // compiler drain the memory counter at the branch join); finish() ignores the items past the
+    // end.  `fast` is block-uniform (the larger concat source decides).
+    const int imax = cpg * (CB > 0 ? max(f.tilesA, f.tilesB) : f.tilesA);
+    fast = imax <= GK * tpg;
 #pragma unroll
     for (int k = 0; k < GK; ++k) {
-      const int i = sub + k * tpg;
-      v[k] = make_float2(0.f, 0.f);
-      if (fast && grp < f.G && i < items) {
-        const int c = fdivi(i, rt), t = i - c * tiles;
-        v[k] = *(const float2*)(base + ((size_t)t * Cs + cs0 + c) * 2);
-      }
+      const int i = min(sub + k * tpg, items - 1);
+      const int c = fdivi(i, rt), t = i - c * tiles;
+      const int off = (t * Cs + cs0 + c) * 2;         // 32-bit offsets: no 64-bit address math
+      v[k] = *(const float2*)(base + off);
     }
+    const int cg = c0 + min(sub, cpg - 1);            // clamped: unconditional loads
+    gm = f.gamma[cg];
+    bt = f.beta[cg];
   }
 
   __device__ __forceinline__ void finish(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
@@ -202,26 +208,36 @@ struct GNLoad {
     }
     if (grp >= f.G) return;
     const int cpg = (CA + CB) / f.G, c0 = grp * cpg;
-    double s = 0.0;
+    // fp32 Chan combination of equal-count tiles in a fixed order (items of one thread, then
+    // the xor-butterfly over the group's threads): deterministic, and accurate to ~1e-7
+    // relative since only tile sums and tile-centred M2 are added
+    float s = 0.f;
 #pragma unroll
-    for (int k = 0; k < GK; ++k) s += (double)v[k].x;
+    for (int k = 0; k < GK; ++k)
+      if (sub + k * tpg < items) s += v[k].x;
     for (int o = 1; o < tpg; o <<= 1) s += __shfl_xor(s, o);
-    const double n_tot = (double)items * ntile;
-    const double mean = s / n_tot;
-    double m2 = 0.0;
+    const float n_tot = (float)items * (float)ntile;
+    const float r_tot = 1.0f / n_tot, r_tile = 1.0f / (float)ntile, fn = (float)ntile;
+    const float mean = s * r_tot;
+    float m2 = 0.f;
 #pragma unroll
     for (int k = 0; k < GK; ++k) {
       if (sub + k * tpg < items) {
-        const double d = (double)v[k].x / ntile - mean;
-        m2 += (double)v[k].y + (double)ntile * d * d;
+        const float d = v[k].x * r_tile - mean;
+        m2 += v[k].y + fn * d * d;
       }
     }
     for (int o = 1; o < tpg; o <<= 1) m2 += __shfl_xor(m2, o);
-    const double rstd = 1.0 / sqrt(m2 / n_tot + (double)f.eps);
-    for (int c = sub; c < cpg; c += tpg) {
-      const double scale = (double)f.gamma[c0 + c] * rstd;
-      sc[c0 + c] = (float)scale;
-      sh[c0 + c] = (float)((double)f.beta[c0 + c] - mean * scale);
+    const float rstd = 1.0f / sqrtf(m2 * r_tot + f.eps);
+    if (sub < cpg) {
+      const float scale = gm * rstd;
+      sc[c0 + sub] = scale;
+      sh[c0 + sub] = bt - mean * scale;
+    }
+    for (int c = sub + tpg; c < cpg; c += tpg) {
+      const float scale = f.gamma[c0 + c] * rstd;
+      sc[c0 + c] = scale;
+      sh[c0 + c] = f.beta[c0 + c] - mean * scale;
     }
   }
 };

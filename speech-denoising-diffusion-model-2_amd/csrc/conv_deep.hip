@@ -4,25 +4,26 @@
 // there, and any wide layer whose input does not fit the row-streaming kernel.
 //
 // These layers are small GEMMs (M = B*pixels = 512..32768, N = Cout = 64..160, K = 9*Cin up to
-// 2880 + the 1x1 res_conv) whose cost is latency and instruction issue, not bandwidth.  A block
-// (4 waves, two blocks per CU so one block's staging overlaps the other's MFMAs) owns MT output
-// pixels of one image x 32 output channels and
-//   1. issues, before anything waits: the first weight fragments of every wave, the producer's
-//      GroupNorm tile statistics and the raw input halo of all input channels (plus the raw
-//      ResnetBlock.res_conv input), every load unconditional (clamped addresses) so the
-//      compiler keeps them all in flight;
+// 2880 + the 1x1 res_conv) whose cost is memory latency and instruction issue, not bandwidth:
+// a block's time is the length of its chain of dependent memory round trips.  The kernel is
+// therefore built so that a block waits on memory ONCE:
+//   1. before anything waits it issues, in the order they are needed: the producer's GroupNorm
+//      tile statistics + gamma / beta, the raw input halo of all input channels (+ the raw
+//      ResnetBlock.res_conv input and the identity-residual tile), bias + noise embedding, and
+//      the weight fragments of the wave's first D K-steps (all of its K-steps when they fit) —
+//      every load unconditional (clamped addresses) and the first staging pass straight-line
+//      code, so the compiler's vmcnt accounting keeps them all in flight;
 //   2. finalizes GroupNorm (fp64 Chan combination, fixed order), applies GN + SiLU, resolves the
 //      nearest upsample / stride-2 halo / virtual channel concat / zero padding, and writes a
 //      plane-major LDS image (a plane = one 16-byte channel unit of every halo pixel; plane
-//      stride = 0 mod 256 B so the ds_read_b128 lane groups of an MFMA operand never collide;
-//      staging writes go 8 consecutive pixels of one plane per 8-lane group, conflict free);
-//   3. splits K (taps x 32-channel chunks, then the res_conv chunks) round-robin over the 4 waves;
-//      each wave streams its weight fragments from L2 through a D-deep register ring while the
-//      pixel fragments come from LDS;
-//   4. reduces the 4 partial tiles through LDS in a fixed order (deterministic), adds bias +
-//      noise embedding + identity residual, stores 4-channel vectors, and reduces the GroupNorm
-//      statistics of the stored values from registers (shuffles + one LDS exchange).
-// If the input does not fit in LDS the chunks are processed in batches (one round trip each).
+//      stride = 0 mod 256 B so the ds_read_b128 lane groups of an MFMA operand never collide);
+//   3. splits K (taps x 32-channel chunks, then the res_conv chunks) round-robin over the NW
+//      waves; pixel fragments come from LDS, weight fragments from the register ring;
+//   4. reduces the NW partial tiles through LDS in a fixed order (deterministic), adds bias +
+//      noise embedding + identity residual (both parked in LDS by step 1), stores 4-channel
+//      vectors, and reduces the GroupNorm statistics of the stored values from registers.
+// NW = 8 (one block per CU, K split 8 ways) keeps a large K resident for the small late-level
+// grids; NW = 4 (two blocks per CU) overlaps two blocks' round trips on the larger grids.
 #include "conv_common.h"
 #include "kernels.h"
 
@@ -40,6 +41,27 @@ __host__ __device__ inline DeepGeo deep_geo(bool s2, int TR, int TW, int MT) {
   return d;
 }
 
+// LDS byte layout of one block; region 0 (the staged image) is reused for the partial tiles
+struct DeepLds { int rres, badd, gsc, total; };
+
+template <typename T, int MT, int NW>
+__host__ __device__ inline DeepLds deep_layout(const DeepGeo& g, int nck, int rck, int Cin, bool ident) {
+  constexpr int ES = (int)sizeof(T), UPP = 2 * ES, NBP = 36;
+  constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;   // two-stage reduction for 8 x 128 pixels
+  const int red = SLOTS * MT * NBP * 4;
+  const int stage = nck * UPP * g.PLB + rck * UPP * g.PLR;
+  DeepLds L;
+  int off = stage > red ? stage : red;
+  L.rres = off;
+  off += ident ? MT * 32 * ES : 0;
+  L.badd = off;
+  off += 32 * 4;
+  L.gsc = off;
+  off += 2 * Cin * 4;
+  L.total = off;
+  return L;
+}
+
 // Chan merge of (n, mean, M2) partial statistics
 __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, float nb, float meanb, float m2b) {
   const float nt = n + nb;
@@ -51,15 +73,16 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   n = nt;
 }
 
-template <typename T, bool S2, int MT>
-__global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
+template <typename T, bool S2, int MT, int NW, int D>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) {
+  constexpr int NT = 64 * NW;
   constexpr int ES = (int)sizeof(T);
   constexpr int UPP = 2 * ES;          // 16-byte planes per 32-channel chunk
   constexpr int UPL = ES / 2;          // planes per MFMA lane group (8 channels)
   constexpr int VE = 16 / ES;          // channels per plane
   constexpr int FP = MT / 16, FC = 2, NB = 32, NBP = NB + 4;
-  constexpr int MAXU = 8;              // staged 16-byte units per thread per round trip
-  constexpr int D = (ES == 4 ? 4 : 8) / (MT >= 128 ? 2 : 1);   // weight-fragment ring depth
+  constexpr int MAXU = ES == 4 ? (NW == 8 ? 6 : 8) : (NW == 8 ? 10 : 16);   // units per thread per pass
+  constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
@@ -72,31 +95,155 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
   const int HC = geo.HC, HP = geo.HP, PLB = geo.PLB, PLR = geo.PLR;
   const int Cin = a.CA + a.CB, nck = Cin / 32;
   const int RC = a.RCA + a.RCB, rck = a.res_mode == 2 ? RC / 32 : 0;
-  const int CBT = a.ck_batch;
-  const bool gn = a.gamma != nullptr;
-  const int res_off = CBT * UPP * PLB;
-  float* gsc = (float*)(smem + res_off + rck * UPP * PLR);   // [2][Cin]
-  const int img_in = a.Hi * a.Wi;
+  const bool gn = a.gamma != nullptr, ident = a.res_mode == 1;
+  const DeepLds lay = deep_layout<T, MT, NW>(geo, nck, rck, Cin, ident);
+  float* gsc = (float*)(smem + lay.gsc);                 // [2][Cin] GroupNorm scale / shift
+  const int res_off = nck * UPP * PLB;
+  const int img_in = a.Hi * a.Wi, img_out = a.Ho * a.Wo;
   const T* srcA = (const T*)a.srcA + (size_t)b * img_in * a.CA;
   const T* srcB = a.CB ? (const T*)a.srcB + (size_t)b * img_in * a.CB : srcA;
-  const int img_out = a.Ho * a.Wo;
   const T* rawA = a.res_mode == 2 ? (const T*)a.rawA + (size_t)b * img_out * a.RCA : srcA;
   const T* rawB = (a.res_mode == 2 && a.RCB) ? (const T*)a.rawB + (size_t)b * img_out * a.RCB : rawA;
+  const T* rsrc = ident ? (const T*)a.res_src + (size_t)b * img_out * a.Cout + n0 : srcA;
   SDDM_STAMP(a, 0);
 
-  // epilogue constants of this thread's 4 output channels (fixed for the whole block)
-  const int ec4 = (tid & 7) * 4;
-  float badd[4];
-  {
-    const int t_now = a.t_dev ? *a.t_dev : 0;
-    const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : nullptr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) badd[i] = a.bias[n0 + ec4 + i] + (trow ? trow[n0 + ec4 + i] : 0.f);
-  }
+  // ---------------- 1. issue every load of the block ----------------
   GNLoad gl;
   const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
   if (gn) gl.issue(gf, b, a.CA, a.CB);
 
+  // staging units: [0, n3) halo planes (8 lanes = 8 consecutive halo pixels of one plane),
+  // [n3, n3 + nres) raw res_conv input at the output pixels, then the identity-residual tile
+  const int nq3 = nck * UPP;
+  const int n3 = (HP + 7) / 8 * 8 * nq3;
+  const int nqr = rck * UPP;
+  const int nres = nqr * MT;
+  const int total = n3 + nres + (ident ? MT * UPP : 0);
+  const float rnq3 = 1.0f / (float)max(nq3, 1), rnqr = 1.0f / (float)max(nqr, 1);
+  const float rHC = 1.0f / (float)HC, rTW = 1.0f / (float)a.TW;
+  // packed destination: LDS byte offset << 10 | (GroupNorm channel + 2); -2 = zero, -1 = raw copy
+  auto unit = [&](int u, f32x4& r, int& pk) {
+    const T* ptr = srcA;               // any valid address; the value is unused when pk < 0
+    int d = -1, gs = -1;
+    if (u < n3) {
+      const int grp = u >> 3, gq = fdivi(grp, rnq3), q = grp - gq * nq3, hp = gq * 8 + (u & 7);
+      const int hy = fdivi(hp, rHC), hx = hp - hy * HC;
+      int iy, ix;
+      bool ok;
+      if (S2) {
+        iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
+        ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+      } else {
+        iy = y0 - 1 + hy; ix = x0 - 1 + hx;
+        ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
+        if (a.upsample) { iy >>= 1; ix >>= 1; }
+      }
+      const int c = q * VE;
+      const bool fromA = c < a.CA;
+      if (ok) ptr = (fromA ? srcA : srcB) + (iy * a.Wi + ix) * (fromA ? a.CA : a.CB) + (fromA ? c : c - a.CA);
+      if (hp < HP) { d = q * PLB + hp * 16; gs = ok ? c : -2; }
+    } else if (u < n3 + nres) {
+      const int v = u - n3, grp = v >> 3, gq = fdivi(grp, rnqr), q = grp - gq * nqr, p = gq * 8 + (v & 7);
+      d = res_off + q * PLR + p * 16;
+      gs = -2;
+      if (p < npv) {
+        const int py = fdivi(p, rTW), px = p - py * a.TW;
+        const int c = q * VE;
+        const bool fromA = c < a.RCA;
+        ptr = (fromA ? rawA : rawB) + ((y0 + py) * a.Wo + (x0 + px)) * (fromA ? a.RCA : a.RCB) +
+              (fromA ? c : c - a.RCA);
+        gs = -1;
+      }
+    } else if (u < total) {            // identity residual [p][32 channels]
+      const int v = u - n3 - nres, p = v / UPP, q = v - p * UPP;
+      d = lay.rres + v * 16;
+      gs = -2;
+      if (p < npv) {
+        const int py = fdivi(p, rTW), px = p - py * a.TW;
+        ptr = rsrc + ((y0 + py) * a.Wo + (x0 + px)) * a.Cout + q * VE;
+        gs = -1;
+      }
+    }
+    r = *(const f32x4*)ptr;
+    pk = d < 0 ? -1 : (d << 10) | (gs + 2);
+  };
+  auto commit = [&](const f32x4& r, int pk) {
+    if (pk < 0) return;
+    const int gs = (pk & 1023) - 2;
+    f32x4 v = r;
+    if (gs == -2) v = f32x4{0.f, 0.f, 0.f, 0.f};
+    else if (gn && gs >= 0 && !(a.dbg & 2)) v = transform_lds<T>(v, gsc + gs, gsc + Cin + gs);
+    *(f32x4*)(smem + (pk >> 10)) = v;
+  };
+  // the first pass: nu0 (block-uniform) units per thread; a uniform branch skips the rest
+  const int nu0 = min((total + NT - 1) / NT, MAXU);
+  f32x4 reg[MAXU];
+  int pk[MAXU];
+#pragma unroll
+  for (int k = 0; k < MAXU; ++k) {
+#ifdef SDDM_DEEP_GUARD
+    pk[k] = -1;
+    if (k < nu0)
+#endif
+    unit(tid + k * NT, reg[k], pk[k]);
+    if (a.dbg & 4) pk[k] = -1;
+  }
+
+  // the step counter selecting the noise-embedding row (loaded with everything else; the
+  // bias + embedding loads that depend on it are issued after the staging wait)
+  const int t_now = a.t_dev ? *a.t_dev : 0;
+
+  // this wave's K steps (wave-uniform) and the first D weight fragments of each
+  const int ns3 = nck * 9, ns = ns3 + rck;
+  const int nj = wv < ns ? (ns - wv + NW - 1) / NW : 0;
+  const int s_last = wv + NW * max(nj - 1, 0);
+  const size_t w3 = (size_t)nck * 9 * 32;                // elements per packed 3x3 weight row
+  const T* wbase = (const T*)a.wgt + (size_t)(n0 + (lane & 15)) * w3 + g * 8;
+  const T* rbase = (const T*)a.res_wgt + (size_t)(n0 + (lane & 15)) * RC + g * 8 - (size_t)ns3 * 32;
+  auto wfrag = [&](int s, int fc) -> Frag<T> {
+    const T* p = s < ns3 ? wbase + (size_t)fc * 16 * w3 + (size_t)s * 32 : rbase + (size_t)fc * 16 * RC + (size_t)s * 32;
+    return load_frag<T>((const char*)p);
+  };
+  Frag<T> wa[D][FC];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#ifdef SDDM_DEEP_GUARD
+    if (d < nj)                                          // wave-uniform
+#endif
+    {
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) wa[d][fc] = (a.dbg & 32) ? Frag<T>{} : wfrag(min(wv + NW * d, s_last), fc);
+    }
+  SDDM_STAMP(a, 1);
+
+  // ---------------- 2. GroupNorm finalize, GN + SiLU into the LDS image ----------------
+  if (gn && !(a.dbg & 1)) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
+  __syncthreads();                                       // scale / shift visible
+  SDDM_STAMP(a, 2);
+#pragma unroll
+  for (int k = 0; k < MAXU; ++k)
+#ifdef SDDM_DEEP_GUARD
+    if (k < nu0)
+#endif
+    commit(reg[k], pk[k]);
+  for (int u0 = MAXU * NT; u0 < total; u0 += MAXU * NT) {   // inputs larger than one pass
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) unit(u0 + tid + k * NT, reg[k], pk[k]);
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) commit(reg[k], pk[k]);
+  }
+  __syncthreads();
+  SDDM_STAMP(a, 3);
+  // bias + noise embedding of this thread's 4 epilogue channels: in flight during the K loop
+  const int ec4 = (tid & 7) * 4;
+  float bb[4];
+  {
+    const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : nullptr;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bb[i] = a.bias[n0 + ec4 + i] + (trow ? trow[n0 + ec4 + i] : 0.f);
+  }
+
+  // ---------------- 3. this wave's K steps ----------------
   int pix_off[FP];
 #pragma unroll
   for (int fp = 0; fp < FP; ++fp) {
@@ -110,155 +257,68 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
   for (int i = 0; i < FP; ++i)
 #pragma unroll
     for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  const size_t w3 = (size_t)nck * 9 * 32;              // elements per packed 3x3 weight row
-  const float rHC = 1.0f / (float)HC, rTW = 1.0f / (float)a.TW;
-  const int nbatch = (nck + CBT - 1) / CBT;
-  bool gn_pending = gn;
-  for (int bi = 0; bi < nbatch; ++bi) {
-    const int c_lo = bi * CBT, c_hi = min(nck, c_lo + CBT);
-    const bool last = bi == nbatch - 1;
-    const int nq3 = (c_hi - c_lo) * UPP;
-    const int n3 = (HP + 7) / 8 * 8 * nq3;
-    const int nqr = last ? rck * UPP : 0;
-    const int total = n3 + nqr * MT;
-    const float rnq3 = 1.0f / (float)max(nq3, 1), rnqr = 1.0f / (float)max(nqr, 1);
-    // ---- this batch's K steps (wave-uniform, SGPRs) and the first D weight fragments ----
-    const int ns3 = (c_hi - c_lo) * 9;
-    const int ns = ns3 + nqr / UPP;
-    const int nj = (wv < ns && !(a.dbg & 8)) ? (ns - wv + 3) / 4 : 0;
-    const int s_last = wv + 4 * max(nj - 1, 0);
-    const T* wbase = (const T*)a.wgt + (size_t)(n0 + (lane & 15)) * w3 + (size_t)c_lo * 9 * 32 + g * 8;
-    const T* rbase = (const T*)a.res_wgt + (size_t)(n0 + (lane & 15)) * RC + g * 8;
-    auto wfrag = [&](int s, int fc) -> Frag<T> {
-      if (s < ns3) return load_frag<T>((const char*)(wbase + (size_t)fc * 16 * w3 + (size_t)s * 32));
-      return load_frag<T>((const char*)(rbase + (size_t)fc * 16 * RC + (s - ns3) * 32));
-    };
-    Frag<T> wa[D][FC];
-    if (nj > 0) {
+  const int nj_run = (a.dbg & 8) ? 0 : nj;
+  for (int j0 = 0; j0 < nj_run; j0 += D) {
+    const bool refill = j0 + D < nj;                     // the ring wraps (K longer than D steps)
 #pragma unroll
-      for (int d = 0; d < D; ++d)
+    for (int d = 0; d < D; ++d) {
+      const int j = j0 + d;
+      const int s = wv + NW * j;
+      if (j < nj) {
+        Frag<T> bf[FP];
+        if (s < ns3) {
+          const int lc = s / 9, tap = s - 9 * lc, dy = tap / 3, dx = tap - 3 * dy;
+          const char* pb = smem + (lc * UPP + g * UPL) * PLB + (dy * HC + dx) * 16;
 #pragma unroll
-        for (int fc = 0; fc < FC; ++fc) wa[d][fc] = wfrag(min(wv + 4 * d, s_last), fc);
-    }
-    if (bi > 0) __syncthreads();                       // previous batch's readers are done
-    // ---------------- staging: global -> registers -> (GN + SiLU) -> LDS ----------------
-    for (int u0 = 0; u0 < total; u0 += MAXU * 256) {
-      f32x4 reg[MAXU];
-      int dst[MAXU], gsel[MAXU];
+          for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(pb + pix_off[fp], PLB);
+        } else {
+          const char* pb = smem + res_off + ((s - ns3) * UPP + g * UPL) * PLR + (lane & 15) * 16;
 #pragma unroll
-      for (int k = 0; k < MAXU; ++k) {
-        const int u = u0 + tid + k * 256;
-        const T* ptr = srcA;                           // any valid address; result unused if dst < 0
-        int d = -1, gs = -1;
-        if (u < n3) {                                  // 8 lanes = 8 consecutive halo pixels of one plane
-          const int grp = u >> 3, gq = fdivi(grp, rnq3), q = grp - gq * nq3, hp = gq * 8 + (u & 7);
-          const int hy = fdivi(hp, rHC), hx = hp - hy * HC;
-          int iy, ix;
-          bool ok;
-          if (S2) {
-            iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
-            ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
-          } else {
-            iy = y0 - 1 + hy; ix = x0 - 1 + hx;
-            ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
-            if (a.upsample) { iy >>= 1; ix >>= 1; }
-          }
-          const int c = c_lo * 32 + q * VE;
-          const bool fromA = c < a.CA;
-          if (ok) ptr = (fromA ? srcA : srcB) + (iy * a.Wi + ix) * (fromA ? a.CA : a.CB) + (fromA ? c : c - a.CA);
-          if (hp < HP) { d = q * PLB + hp * 16; gs = ok ? c : -2; }
-        } else if (u < total) {                        // raw res_conv input at the output pixels
-          const int v = u - n3, grp = v >> 3, gq = fdivi(grp, rnqr), q = grp - gq * nqr, p = gq * 8 + (v & 7);
-          d = res_off + q * PLR + p * 16;
-          gs = -2;
-          if (p < npv) {
-            const int py = fdivi(p, rTW), px = p - py * a.TW;
-            const int c = q * VE;
-            const bool fromA = c < a.RCA;
-            ptr = (fromA ? rawA : rawB) + ((y0 + py) * a.Wo + (x0 + px)) * (fromA ? a.RCA : a.RCB) +
-                  (fromA ? c : c - a.RCA);
-            gs = -1;
-          }
-        }
-        reg[k] = *(const f32x4*)ptr;
-        dst[k] = d;
-        gsel[k] = gs;
-      }
-      SDDM_STAMP(a, 1);
-      if (gn_pending) {
-        gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
-        gn_pending = false;
-        __syncthreads();                               // scale / shift visible
-      }
-      SDDM_STAMP(a, 2);
-#pragma unroll
-      for (int k = 0; k < MAXU; ++k) {
-        if (dst[k] < 0) continue;
-        f32x4 v = reg[k];
-        if (gsel[k] == -2) v = f32x4{0.f, 0.f, 0.f, 0.f};                 // zero padding
-        else if (gn && gsel[k] >= 0) v = transform_lds<T>(v, gsc + gsel[k], gsc + Cin + gsel[k]);
-        *(f32x4*)(smem + dst[k]) = v;
-      }
-    }
-    __syncthreads();
-    SDDM_STAMP(a, 3);
-    // ---------------- this wave's K steps: round-robin over the 4 waves ----------------
-    // every ring refill is unconditional (clamped to the wave's last step) so the compiler's
-    // vmcnt accounting keeps D fragment loads in flight
-    for (int j0 = 0; j0 < nj; j0 += D) {
-#pragma unroll
-      for (int d = 0; d < D; ++d) {
-        const int j = j0 + d;
-        const int s = wv + 4 * j;
-        if (j < nj) {
-          Frag<T> bf[FP];
-          if (s < ns3) {
-            const int lc = s / 9, tap = s - 9 * lc, dy = tap / 3, dx = tap - 3 * dy;
-            const char* pb = smem + (lc * UPP + g * UPL) * PLB + (dy * HC + dx) * 16;
-#pragma unroll
-            for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(pb + pix_off[fp], PLB);
-          } else {
-            const char* pb = smem + res_off + ((s - ns3) * UPP + g * UPL) * PLR + (lane & 15) * 16;
-#pragma unroll
-            for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(pb + fp * 256, PLR);
-          }
-#pragma unroll
-          for (int fc = 0; fc < FC; ++fc)
-#pragma unroll
-            for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], wa[d][fc], bf[fp]);
+          for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(pb + fp * 256, PLR);
         }
 #pragma unroll
-        for (int fc = 0; fc < FC; ++fc) wa[d][fc] = wfrag(min(s + 4 * D, s_last), fc);
-      }
-    }
-  }
-  // identity residual of this thread's output pixels: issued before the reduction barrier
-  constexpr int PPI = 256 / (NB / 4);                 // pixels per epilogue pass (32)
-  constexpr int EIT = (MT + PPI - 1) / PPI;
-  typedef T vec4 __attribute__((ext_vector_type(4)));
-  vec4 rres[EIT];
-  if (a.res_mode == 1) {
-    const T* rs = (const T*)a.res_src + (size_t)b * img_out * a.Cout + n0 + ec4;
+        for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
-    for (int it = 0; it < EIT; ++it) {
-      int p = it * PPI + (tid >> 3);
-      if (p >= npv) p = 0;
-      const int py = fdivi(p, rTW), px = p - py * a.TW;
-      rres[it] = *(const vec4*)(rs + ((y0 + py) * a.Wo + (x0 + px)) * a.Cout);
+          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], wa[d][fc], bf[fp]);
+      }
+      if (refill) {
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) wa[d][fc] = wfrag(min(s + NW * D, s_last), fc);
+      }
     }
   }
   SDDM_STAMP(a, 4);
-  __syncthreads();
-  // ---------------- reduce the 4 partial tiles: red[wave][MT][NBP] ----------------
+
+  // ---------------- 4. reduce the partial tiles: red[slot][MT][NBP] ----------------
+  __syncthreads();                                       // every wave is done with the image
   float* red = (float*)smem;
+  auto put = [&](int slot) {
 #pragma unroll
-  for (int fp = 0; fp < FP; ++fp) {
-    const int p = fp * 16 + (lane & 15);
+    for (int fp = 0; fp < FP; ++fp) {
+      const int p = fp * 16 + (lane & 15);
 #pragma unroll
-    for (int fc = 0; fc < FC; ++fc) *(f32x4*)(red + (wave * MT + p) * NBP + fc * 16 + 4 * g) = acc[fp][fc];
+      for (int fc = 0; fc < FC; ++fc) *(f32x4*)(red + (slot * MT + p) * NBP + fc * 16 + 4 * g) = acc[fp][fc];
+    }
+  };
+  if (SLOTS < NW) {                                      // waves 4..7 into slots, waves 0..3 add theirs
+    if (wv >= SLOTS) put(wv - SLOTS);
+    __syncthreads();
+    if (wv < SLOTS) {
+#pragma unroll
+      for (int fp = 0; fp < FP; ++fp) {
+        const int p = fp * 16 + (lane & 15);
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) acc[fp][fc] += *(const f32x4*)(red + (wv * MT + p) * NBP + fc * 16 + 4 * g);
+      }
+      put(wv);
+    }
+  } else {
+    put(wv);
   }
   __syncthreads();
+
+  constexpr int PPI = NT / 8;                            // pixels per epilogue pass
+  constexpr int EIT = (MT + PPI - 1) / PPI;
   float sn = 0.f, sk[4], s1[4], s2[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) { sk[i] = 0.f; s1[i] = 0.f; s2[i] = 0.f; }
@@ -270,13 +330,14 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
       const int py = fdivi(p, rTW), px = p - py * a.TW;
       f32x4 s = *(const f32x4*)(red + p * NBP + ec4);
 #pragma unroll
-      for (int w = 1; w < 4; ++w) s += *(const f32x4*)(red + (w * MT + p) * NBP + ec4);
+      for (int w = 1; w < SLOTS; ++w) s += *(const f32x4*)(red + (w * MT + p) * NBP + ec4);
       float v[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = s[i] + badd[i];
-      if (a.res_mode == 1) {
+      for (int i = 0; i < 4; ++i) v[i] = s[i] + bb[i];
+      if (ident) {
+        const T* rp = (const T*)(smem + lay.rres) + p * 32 + ec4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] += (float)rres[it][i];
+        for (int i = 0; i < 4; ++i) v[i] += to_f32<T>(rp[i]);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) v[i] = round_t<T>(v[i]);
@@ -295,10 +356,11 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
     }
   }
   SDDM_STAMP(a, 5);
-  if (a.stats) {
-    // per-thread (n, mean, M2) -> lanes of one channel group (xor 8, 16, 32) -> 4 waves via LDS;
-    // full tiles give every thread the same count, so the merges need no division
-    const bool even = (npv & (PPI - 1)) == 0;
+  if (a.stats && !(a.dbg & 16)) {
+    // per-thread (n, mean, M2) -> lanes of one channel group (xor 8, 16, 32) -> waves via LDS;
+    // a full tile gives every epilogue thread the same count, so the merges need no division
+    constexpr int NWE = (MT / 8 < NW) ? MT / 8 : NW;    // waves holding epilogue pixels
+    const bool even = npv == MT;
     float mn[4], m2[4], nn = sn;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -330,8 +392,8 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
       nn = nv[0];
     }
     __syncthreads();                                   // red reads done
-    float* xs = red;                                   // [4 waves][8 groups][4 ch][3]
-    if (lane < 8)
+    float* xs = red;                                   // [NWE waves][8 groups][4 ch][3]
+    if (wv < NWE && lane < 8)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float* e = xs + ((wave * 8 + lane) * 4 + i) * 3;
@@ -341,7 +403,7 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
     if (tid < NB) {
       const int grp = tid >> 2, i = tid & 3;
       float n = 0.f, mean = 0.f, q = 0.f;
-      for (int w = 0; w < 4; ++w) {
+      for (int w = 0; w < NWE; ++w) {
         const float* e = xs + ((w * 8 + grp) * 4 + i) * 3;
         chan_merge(n, mean, q, e[0], e[1], e[2]);
       }
@@ -354,53 +416,70 @@ __global__ __launch_bounds__(256, 2) void conv_deep_kernel(ConvArgs a) {
   SDDM_STAMP(a, 7);
 }
 
-template <typename T, bool S2, int MT>
-static size_t deep_lds(const ConvArgs& a, int ck_batch) {
-  constexpr int ES = (int)sizeof(T), UPP = 2 * ES;
-  const DeepGeo geo = deep_geo(S2, a.TR, a.TW, MT);
-  const int Cin = a.CA + a.CB, rck = a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0;
-  const size_t stage = (size_t)ck_batch * UPP * geo.PLB + (size_t)rck * UPP * geo.PLR + (size_t)2 * Cin * 4;
-  const size_t red = (size_t)4 * MT * (32 + 4) * 4;
-  return stage > red ? stage : red;
+// weight-ring depth for a wave's K steps: the whole K when it fits in the register budget
+template <typename T, int MT, int NW>
+static int deep_ring(int steps_per_wave) {
+  if (sizeof(T) == 4 || NW == 4) return 8 / (int)(sizeof(T) == 4 ? 2 : 1);
+  if (steps_per_wave <= 8 || MT >= 128) return 8;
+  return 12;
 }
 
-template <typename T, bool S2, int MT>
+template <typename T, bool S2, int MT, int NW>
 static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
+  const int nck = (a.CA + a.CB) / 32, rck = a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0;
+  const DeepGeo geo = deep_geo(S2, a.TR, a.TW, MT);
+  const DeepLds lay = deep_layout<T, MT, NW>(geo, nck, rck, a.CA + a.CB, a.res_mode == 1);
   if (lo) {
-    *lo = deep_lds<T, S2, MT>(a, a.ck_batch);
+    *lo = (size_t)lay.total;
     return hipSuccess;
   }
-  const int nck = (a.CA + a.CB) / 32;
-  if (a.ck_batch < 1 || a.ck_batch > nck || a.TR * a.TW > MT || a.Cout % 32 || (a.CA + a.CB) % 32)
+  if (a.TR * a.TW > MT || a.Cout % 32 || (a.CA + a.CB) % 32 || (a.CA + a.CB) > 1000 || (a.RCA + a.RCB) % 32)
     return hipErrorInvalidValue;
-  const size_t lds = deep_lds<T, S2, MT>(a, a.ck_batch);
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT>), dim3(a.n_tiles, B, a.Cout / 32), dim3(256), lds, s, a);
-  return hipGetLastError();
+  if (lay.total > 160 * 1024) return hipErrorInvalidValue;
+  const dim3 grid(a.n_tiles, B, a.Cout / 32), blk(64 * NW);
+  const int D = deep_ring<T, MT, NW>((nck * 9 + rck + NW - 1) / NW);
+#define SDDM_RING(DV)                                                                         \
+  if (D == DV) {                                                                              \
+    hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT, NW, DV>), grid, blk, lay.total, s, a);   \
+    return hipGetLastError();                                                                 \
+  }
+  if constexpr (sizeof(T) == 4) {
+    SDDM_RING(4)
+  } else if constexpr (NW == 4 || MT >= 128) {
+    SDDM_RING(8)
+  } else {
+    SDDM_RING(8) SDDM_RING(12)
+  }
+#undef SDDM_RING
+  return hipErrorInvalidValue;
 }
 
 template <typename T>
-static hipError_t deep_dispatch(int mt, bool s2, const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
-#define SDDM_DEEP(S2V, MTV) \
-  if (s2 == S2V && mt == MTV) return deep_go<T, S2V, MTV>(a, B, s, lo);
-  SDDM_DEEP(false, 32) SDDM_DEEP(false, 64) SDDM_DEEP(false, 128)
-  SDDM_DEEP(true, 32) SDDM_DEEP(true, 64) SDDM_DEEP(true, 128)
+static hipError_t deep_dispatch(int mt, int nw, bool s2, const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
+#define SDDM_DEEP(S2V, MTV, NWV) \
+  if (s2 == S2V && mt == MTV && nw == NWV) return deep_go<T, S2V, MTV, NWV>(a, B, s, lo);
+  SDDM_DEEP(false, 32, 4) SDDM_DEEP(false, 64, 4) SDDM_DEEP(false, 128, 4)
+  SDDM_DEEP(true, 32, 4) SDDM_DEEP(true, 64, 4) SDDM_DEEP(true, 128, 4)
+  SDDM_DEEP(false, 32, 8) SDDM_DEEP(false, 64, 8) SDDM_DEEP(false, 128, 8)
+  SDDM_DEEP(true, 32, 8) SDDM_DEEP(true, 64, 8) SDDM_DEEP(true, 128, 8)
 #undef SDDM_DEEP
   if (lo) *lo = (size_t)1 << 40;
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B, hipStream_t s) {
-  if (dtype == DT_F32) return deep_dispatch<float>(mt, s2, a, B, s, nullptr);
-  if (dtype == DT_BF16) return deep_dispatch<bf16_t>(mt, s2, a, B, s, nullptr);
-  return deep_dispatch<f16_t>(mt, s2, a, B, s, nullptr);
+  const int nw = a.deep_nw;
+  if (dtype == DT_F32) return deep_dispatch<float>(mt, nw, s2, a, B, s, nullptr);
+  if (dtype == DT_BF16) return deep_dispatch<bf16_t>(mt, nw, s2, a, B, s, nullptr);
+  return deep_dispatch<f16_t>(mt, nw, s2, a, B, s, nullptr);
 }
 
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a) {
   size_t lo = (size_t)1 << 40;
-  if (dtype == DT_F32) (void)deep_dispatch<float>(mt, s2, a, 1, 0, &lo);
-  else if (dtype == DT_BF16) (void)deep_dispatch<bf16_t>(mt, s2, a, 1, 0, &lo);
-  else (void)deep_dispatch<f16_t>(mt, s2, a, 1, 0, &lo);
+  const int nw = a.deep_nw;
+  if (dtype == DT_F32) (void)deep_dispatch<float>(mt, nw, s2, a, 1, 0, &lo);
+  else if (dtype == DT_BF16) (void)deep_dispatch<bf16_t>(mt, nw, s2, a, 1, 0, &lo);
+  else (void)deep_dispatch<f16_t>(mt, nw, s2, a, 1, 0, &lo);
   return lo;
 }
 

@@ -126,7 +126,8 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   }
   // row-group prefetch geometry of this thread's units (the same every iteration), and the
   // GroupNorm scale / shift of their channels held in registers
-  int pr[UPT], uoff[UPT], loff[UPT];          // row in group, source offset (elements, +A/B flag), LDS offset
+  // (all per-iteration address math below is 32-bit with 24-bit multiplies: full-rate VALU)
+  int pr[UPT], uoff[UPT], loff[UPT], cq[UPT];  // row in group, source offset (elements, +A/B flag), LDS offset, channel
 #pragma unroll
   for (int k = 0; k < UPT; ++k) {
     const int u = tid + k * NT, grp = u >> 6, j = u & 63;
@@ -134,6 +135,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     const int q = j / PB, x = pix % W;
     pr[k] = pix / W;
     loff[k] = q * PL + (x + 1) * 16;
+    cq[k] = q * VE;
     const int c0 = q * VE;
     const int sx = a.upsample ? (x >> 1) : x;
     const bool fa = c0 < a.CA;
@@ -147,20 +149,20 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       const int ry = min(y0 + j * TR + 1 + pr[k], H - 1);
       const int sy = a.upsample ? (ry >> 1) : ry;
       const bool fb = uoff[k] & 1;
-      dst[k] = *(const f32x4*)((fb ? srcBb : srcAb) + (uoff[k] >> 1) + sy * (fb ? rsB : rsA));
+      dst[k] = *(const f32x4*)((fb ? srcBb : srcAb) + ((uoff[k] >> 1) + (int)__umul24(sy, fb ? rsB : rsA)));
     }
   };
   auto commit_rows = [&](const f32x4 (&src)[UPT], int j) {
+    const int sb = (base + j * TR + 2) % R;             // uniform
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
       const int ry = y0 + j * TR + 1 + pr[k];
       f32x4 v = src[k];
       if (ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
-      else if (gn) {
-        const int c0 = (loff[k] / PL) * VE;
-        v = transform_lds<T>(v, gsc + c0, gsc + CIN + c0);
-      }
-      *(f32x4*)(ring + ((base + j * TR + 2 + pr[k]) % R) * SLOT + loff[k]) = v;
+      else if (gn) v = transform_lds<T>(v, gsc + cq[k], gsc + CIN + cq[k]);
+      int sl = sb + pr[k];
+      sl = sl >= R ? sl - R : sl;
+      *(f32x4*)(ring + (int)__umul24(sl, SLOT) + loff[k]) = v;
     }
   };
   // residual inputs of iteration it (issued one iteration ahead)
@@ -169,10 +171,11 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp) {
       const int yy = min(y0 + it * TR, H - TR) + prow[fp];
+      const int po = (int)__umul24(yy * W + pcol[fp], a.Cout);
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) {
         const int co = min(n0 + fc * 16 + 4 * g, a.Cout - 4);
-        dst[fp][fc] = *(const vec4*)(resb + ((size_t)yy * W + pcol[fp]) * a.Cout + co);
+        dst[fp][fc] = *(const vec4*)(resb + (po + co));
       }
     }
   };
@@ -185,8 +188,8 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       for (int fp = 0; fp < FP; ++fp) {
         const int yy = min(y0 + it * TR, H - TR) + prow[fp];
         const int c0 = min(ck, rck - 1) * 32 + g * 8;
-        const size_t pix = (size_t)yy * W + pcol[fp];
-        const T* sp = c0 < a.RCA ? rawAb + pix * a.RCA + c0 : rawBb + pix * a.RCB + (c0 - a.RCA);
+        const int pix = yy * W + pcol[fp];
+        const T* sp = c0 < a.RCA ? rawAb + ((int)__umul24(pix, a.RCA) + c0) : rawBb + ((int)__umul24(pix, a.RCB) + (c0 - a.RCA));
         dst[ck][fp] = load_frag<T>((const char*)sp);
       }
   };
@@ -206,6 +209,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       const int co = n0 + fc * 16 + 4 * g + i;
       badd[fc][i] = (co < a.Cout) ? a.bias[co] + (trow ? trow[co] : 0.f) : 0.f;
     }
+  T* outb = (T*)a.out + (size_t)b * H * W * a.Cout;
   const char* abase = wl + g * UPL * WPL + (lane & 15) * 16;
   const char* rbase = rw + g * UPL * WPL + (lane & 15) * 16;
 
@@ -229,8 +233,11 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp)
 #pragma unroll
-      for (int dy = 0; dy < 3; ++dy)
-        bptr[fp][dy] = ring + ((s_it + prow[fp] + dy) % R) * SLOT + g * UPL * PL + pcol[fp] * 16;
+      for (int dy = 0; dy < 3; ++dy) {
+        int sl = s_it + prow[fp] + dy;                   // < 2R: one conditional wrap
+        sl = sl >= R ? sl - R : sl;
+        bptr[fp][dy] = ring + (int)__umul24(sl, SLOT) + g * UPL * PL + pcol[fp] * 16;
+      }
 #pragma unroll
     for (int ck = 0; ck < NCK; ++ck) {
 #pragma unroll
@@ -262,7 +269,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     // ---- epilogue: bias + embedding + residual, store, statistics ----
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp) {
-      const size_t po = ((size_t)b * H + y + prow[fp]) * W + pcol[fp];
+      const int po = (int)__umul24((y + prow[fp]) * W + pcol[fp], a.Cout);
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) {
         const int co = n0 + fc * 16 + 4 * g;
@@ -276,7 +283,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] = round_t<T>(v[i]);
-        store4<T>((T*)a.out + po * a.Cout + co, v[0], v[1], v[2], v[3]);
+        store4<T>(outb + (po + co), v[0], v[1], v[2], v[3]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float d = v[i] - badd[fc][i];

@@ -69,9 +69,11 @@ struct ConvArgs {
   const void* res_wgt;        // packed [Cout_pad][RCA+RCB] (T)
   void* out;                  // [B][Ho][Wo][Cout]
   float* stats;               // [B][n_tiles][Cout][2] (sum, M2 about tile mean) or null
-  int ck_batch;               // conv_deep: 32-channel input chunks staged in LDS per round trip
+  int ck_batch;               // (unused: conv_deep stages every input chunk at once)
+  int deep_nw;                // conv_deep: waves per block (4: two blocks per CU, 8: one)
   unsigned long long* stamps; // SDDM_STAMPS builds only: per-block phase timestamps [blocks][8]
-  int dbg;                    // ablation flags for timing experiments (0 in production): 8 = skip the K loop
+  int dbg;                    // ablation flags for timing experiments (0 in production); conv_deep: 1 no GN
+                              // finalize, 2 no GN+SiLU, 4 no staging loads, 8 no K loop, 16 no stats, 32 no weight loads
 };
 
 // ---- whole-K-resident tile convolution for the narrow levels (conv_deep.hip) ----

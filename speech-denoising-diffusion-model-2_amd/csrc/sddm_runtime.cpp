@@ -416,15 +416,23 @@ static int upload_tables(sddm_ctx* c) {
 struct ConvChoice {
   int strip = 0;      // 1: row-streaming kernel (conv_strip.hip), 0: whole-K tile kernel (conv_deep.hip)
   int nblk = 32, SR = 0, mpi = 128;
-  int mt = 0, ckb = 0;                            // conv_deep: pixels per block, chunks per round trip
+  int mt = 0, ckb = 0, nw = 4;                    // conv_deep: pixels per block, input chunks, waves
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
 };
 
-// conv_deep tile: the largest pixel tile (fewest weight re-reads from L2) whose grid still fills
-// the 256 CUs with the whole K resident in LDS; otherwise the tile giving the most blocks.
+// conv_deep tile (pixels per block) and waves per block.  A block's time is dominated by its
+// one memory round trip, so the grid should need as few rounds of resident blocks as possible
+// (256 CUs x 2 blocks at 4 waves, x 1 block at 8 waves); among equal round counts 8 waves (the
+// K split 8 ways, weights resident) and then the smaller tile (less work per block) win.
+// SDDM_DEEP_CFG=mt:nw forces one configuration wherever it fits (experiments).
 static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch) {
-  const int nck = (a.CA + a.CB) / 32, nz = a.Cout / 32;
-  struct Cand { int mt, TR, TW, tiles_x, n_tiles, blocks, ckb; };
+  const int nz = a.Cout / 32;
+  static int force_mt = -1, force_nw = -1;
+  if (force_mt < 0) {
+    force_mt = force_nw = 0;
+    if (const char* e = std::getenv("SDDM_DEEP_CFG")) std::sscanf(e, "%d:%d", &force_mt, &force_nw);
+  }
+  struct Cand { int mt, nw, TR, TW, tiles_x, n_tiles, blocks, rounds; };
   std::vector<Cand> cs;
   for (int mt : {128, 64, 32}) {
     const int TW = std::min(a.Wo, mt);
@@ -433,24 +441,26 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch) {
     if (a.Ho % TR) continue;
     if (TR * TW < mt && mt > 32) continue;        // partial tiles only at the smallest size
     a.TR = TR; a.TW = TW; a.tiles_x = a.Wo / TW; a.n_tiles = a.tiles_x * (a.Ho / TR);
-    int ckb = nck;
-    for (; ckb >= 1; --ckb) {
-      a.ck_batch = ckb;
-      if (conv_deep_lds_bytes(dt, mt, s2, a) <= 160 * 1024) break;
+    for (int nw : {8, 4}) {
+      a.deep_nw = nw;
+      if (conv_deep_lds_bytes(dt, mt, s2, a) > 160 * 1024) continue;
+      const int blocks = a.n_tiles * B * nz, per_round = 256 * (nw == 4 ? 2 : 1);
+      cs.push_back({mt, nw, TR, TW, a.tiles_x, a.n_tiles, blocks, (blocks + per_round - 1) / per_round});
     }
-    if (ckb < 1) continue;
-    cs.push_back({mt, TR, TW, a.tiles_x, a.n_tiles, a.n_tiles * B * nz, ckb});
   }
   if (cs.empty()) return false;
   const Cand* pick = nullptr;
   for (const Cand& c : cs)
-    if (c.blocks >= 256 && c.ckb == nck) { pick = &c; break; }
+    if (c.mt == force_mt && c.nw == force_nw) pick = &c;
   if (!pick) {
     pick = &cs[0];
-    for (const Cand& c : cs)
-      if (c.blocks > pick->blocks || (c.blocks == pick->blocks && c.ckb > pick->ckb)) pick = &c;
+    for (const Cand& c : cs) {
+      if (c.rounds != pick->rounds) { if (c.rounds < pick->rounds) pick = &c; continue; }
+      if (c.nw != pick->nw) { if (c.nw > pick->nw) pick = &c; continue; }
+      if (c.mt < pick->mt) pick = &c;
+    }
   }
-  ch.strip = 0; ch.mt = pick->mt; ch.ckb = pick->ckb;
+  ch.strip = 0; ch.mt = pick->mt; ch.nw = pick->nw; ch.ckb = (a.CA + a.CB) / 32;
   ch.TR = pick->TR; ch.TW = pick->TW; ch.tiles_x = pick->tiles_x; ch.n_tiles = pick->n_tiles;
   return true;
 }
@@ -701,7 +711,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                             x.t_dev = lp->rs.t_dev;
                           }
                           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
-                          x.ck_batch = ch.ckb;
+                          x.ck_batch = ch.ckb; x.deep_nw = ch.nw;
                           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
                         }, st.w + (ch.strip ? "[strip]" : "")});
       {  // flags: 1 no stats, 2 no GroupNorm transform, 4 no residual / embedding, 8 skip the K loop
@@ -715,7 +725,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           if (fl & 4) x.res_mode = 0;
           x.dbg = fl;
           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
-          x.ck_batch = ch.ckb;
+          x.ck_batch = ch.ckb; x.deep_nw = ch.nw;
           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
         };
         (void)base;

@@ -29,7 +29,10 @@ SOURCES = ["kernels.hip", "conv_strip.hip", "conv_deep.hip", "sddm_runtime.cpp",
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SDDM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
-         "-Wno-unused-result"] + (["-DSDDM_STAMPS"] if VARIANT == "stamps" else [])
+         "-Wno-unused-result"] + (["-DSDDM_STAMPS"] if VARIANT.startswith("stamps") else [])
+# experiment variants: extra -D flags for a variant build (e.g. SDDM_EXTRA_DEFS="-DFOO -DBAR")
+if VARIANT:
+    FLAGS += os.environ.get("SDDM_EXTRA_DEFS", "").split()
 
 
 def _deps():
