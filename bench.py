@@ -141,8 +141,16 @@ def main():
         if p["launches"]:
             gbs = p["bytes_per_launch"] / (p["avg_ms"] * 1e-3) / 1e9
             tfs = p["flops_per_launch"] / (p["avg_ms"] * 1e-3) / 1e12
+            # measured HBM bytes per conv launch: the committed PMC summary of the same workload
+            # (tools/gpu_traffic.sh + tools/traffic.py; counters cannot be read from inside this run)
+            traffic, tsrc = None, None
+            tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_traffic.json")
+            if os.path.exists(tf):
+                with open(tf) as fh:
+                    traffic = round(json.load(fh)["bytes_per_launch"])
+                tsrc = "profiles/hbm_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same workload)"
             roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
                         "kernel": "conv3x3_kernel (all UNet 3x3 conv launches)",
                         "avg_launch_ms": round(p["avg_ms"], 5), "launches_timed": p["launches"],
                         "alg_bytes_per_launch": round(p["bytes_per_launch"]),

@@ -280,14 +280,39 @@ namespace sddm {
 
 __device__ __forceinline__ float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// SiLU of two values with packed fp32 arithmetic around the two transcendentals per value:
+// y * 1 / (1 + 2^(-y log2 e))
+__device__ __forceinline__ f32x2 silu2(f32x2 y) {
+  const f32x2 t = y * f32x2{-1.4426950408889634f, -1.4426950408889634f};
+  const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + f32x2{1.f, 1.f};
+  return y * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+}
+
+// GroupNorm affine + SiLU of one 16-byte unit (VE channels), re-rounded to T
 template <typename T>
-__device__ __forceinline__ f32x4 transform_fast(f32x4 raw, const float* sc, const float* sh) {
+__device__ __forceinline__ f32x4 transform_regs(f32x4 raw, const float* s, const float* h) {
   constexpr int VE = 16 / (int)sizeof(T);
   typedef T vec __attribute__((ext_vector_type(VE)));
   vec v = __builtin_bit_cast(vec, raw);
 #pragma unroll
-  for (int j = 0; j < VE; ++j) v[j] = from_f32<T>(silu_fast(to_f32<T>(v[j]) * sc[j] + sh[j]));
+  for (int j = 0; j < VE; j += 2) {
+    const f32x2 x = f32x2{to_f32<T>(v[j]), to_f32<T>(v[j + 1])};
+    const f32x2 o = silu2(x * f32x2{s[j], s[j + 1]} + f32x2{h[j], h[j + 1]});
+    v[j] = from_f32<T>(o.x);
+    v[j + 1] = from_f32<T>(o.y);
+  }
   return __builtin_bit_cast(f32x4, v);
+}
+
+template <typename T>
+__device__ __forceinline__ f32x4 transform_fast(f32x4 raw, const float* sc, const float* sh) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  float s[VE], h[VE];
+#pragma unroll
+  for (int j = 0; j < VE; ++j) { s[j] = sc[j]; h[j] = sh[j]; }
+  return transform_regs<T>(raw, s, h);
 }
 
 // GroupNorm affine + SiLU of one 16-byte unit with the per-channel scale / shift read from LDS
@@ -295,7 +320,6 @@ __device__ __forceinline__ f32x4 transform_fast(f32x4 raw, const float* sc, cons
 template <typename T>
 __device__ __forceinline__ f32x4 transform_lds(f32x4 raw, const float* sc, const float* sh) {
   constexpr int VE = 16 / (int)sizeof(T);
-  typedef T vec __attribute__((ext_vector_type(VE)));
   float s[VE], h[VE];
 #pragma unroll
   for (int j = 0; j < VE; j += 4) {
@@ -303,10 +327,7 @@ __device__ __forceinline__ f32x4 transform_lds(f32x4 raw, const float* sc, const
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s[j + i] = a[i]; h[j + i] = c[i]; }
   }
-  vec v = __builtin_bit_cast(vec, raw);
-#pragma unroll
-  for (int j = 0; j < VE; ++j) v[j] = from_f32<T>(silu_fast(to_f32<T>(v[j]) * s[j] + h[j]));
-  return __builtin_bit_cast(f32x4, v);
+  return transform_regs<T>(raw, s, h);
 }
 
 // an MFMA operand fragment whose 16-byte units sit in consecutive planes `stride` bytes apart

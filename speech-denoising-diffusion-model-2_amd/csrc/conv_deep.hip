@@ -21,7 +21,8 @@
 //      waves; pixel fragments come from LDS, weight fragments from the register ring;
 //   4. reduces the NW partial tiles through LDS in a fixed order (deterministic), adds bias +
 //      noise embedding + identity residual (both parked in LDS by step 1), stores 4-channel
-//      vectors, and reduces the GroupNorm statistics of the stored values from registers.
+//      vectors, and reduces the GroupNorm statistics of the fp32 values (before the storage
+//      rounding) from registers.
 // NW = 8 (one block per CU, K split 8 ways) keeps a large K resident for the small late-level
 // grids; NW = 4 (two blocks per CU) overlaps two blocks' round trips on the larger grids.
 #include "conv_common.h"
@@ -339,8 +340,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 #pragma unroll
         for (int i = 0; i < 4; ++i) v[i] += to_f32<T>(rp[i]);
       }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = round_t<T>(v[i]);
       store4<T>(out + ((y0 + py) * a.Wo + (x0 + px)) * a.Cout, v[0], v[1], v[2], v[3]);
       if (it == 0) {
 #pragma unroll

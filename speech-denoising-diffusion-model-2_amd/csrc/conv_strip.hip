@@ -19,7 +19,7 @@
 // Geometry (W, Cin) is compile-time so no integer division runs per element.
 // The epilogue adds bias, the noise-embedding projection and the residual (identity, or the
 // ResnetBlock 1x1 res_conv as extra MFMAs on raw input fragments loaded straight to registers),
-// stores 4 channels per lane, and accumulates GroupNorm statistics of the stored values in
+// stores 4 channels per lane, and accumulates GroupNorm statistics of the fp32 values in
 // registers (per-lane shifted sums, merged with Chan's formula at the end of the strip).
 #include "conv_common.h"
 #include "kernels.h"
@@ -159,7 +159,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       const int ry = y0 + j * TR + 1 + pr[k];
       f32x4 v = src[k];
       if (ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
-      else if (gn) v = transform_lds<T>(v, gsc + cq[k], gsc + CIN + cq[k]);
+      else if (gn && !(a.dbg & 2)) v = transform_lds<T>(v, gsc + cq[k], gsc + CIN + cq[k]);
       int sl = sb + pr[k];
       sl = sl >= R ? sl - R : sl;
       *(f32x4*)(ring + (int)__umul24(sl, SLOT) + loff[k]) = v;
@@ -240,6 +240,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       }
 #pragma unroll
     for (int ck = 0; ck < NCK; ++ck) {
+      if (a.dbg & 8) break;
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int dy = tap / 3, dx = tap - 3 * dy;
@@ -273,22 +274,20 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) {
         const int co = n0 + fc * 16 + 4 * g;
-        if (co >= a.Cout) continue;
-        float v[4];
+        if (co >= a.Cout || (a.dbg & 16)) continue;
+        // statistics of the fp32 values (before the storage rounding), about the shift badd
+        float d[4];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = acc[fp][fc][i] + badd[fc][i];
+        for (int i = 0; i < 4; ++i) d[i] = acc[fp][fc][i];
         if (a.res_mode == 1) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) v[i] += (float)r1cur[fp][fc][i];
+          for (int i = 0; i < 4; ++i) d[i] += (float)r1cur[fp][fc][i];
         }
-#pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] = round_t<T>(v[i]);
-        store4<T>(outb + (po + co), v[0], v[1], v[2], v[3]);
+        store4<T>(outb + (po + co), d[0] + badd[fc][0], d[1] + badd[fc][1], d[2] + badd[fc][2], d[3] + badd[fc][3]);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float d = v[i] - badd[fc][i];
-          s1[fc][i] += d;
-          s2[fc][i] += d * d;
+          s1[fc][i] += d[i];
+          s2[fc][i] += d[i] * d[i];
         }
       }
     }

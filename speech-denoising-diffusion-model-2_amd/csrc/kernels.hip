@@ -235,15 +235,15 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
     T* op = (T*)a.out + (((size_t)b * F + f0 + r) * W + w) * CO;
 #pragma unroll
     for (int fc = 0; fc < 2; ++fc) {
-      float v[4];
+      // statistics of the fp32 values about the shift = bias (common to the whole tile)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        v[i] = round_t<T>(acc[fc][i] + bias[fc][i]);
-        const float d = v[i] - bias[fc][i];     // shift = bias (common to the whole tile)
+        const float d = acc[fc][i];
         st1[fc][i] += d;
         st2[fc][i] += d * d;
       }
-      store4<T>(op + fc * 16 + 4 * g, v[0], v[1], v[2], v[3]);
+      store4<T>(op + fc * 16 + 4 * g, acc[fc][0] + bias[fc][0], acc[fc][1] + bias[fc][1], acc[fc][2] + bias[fc][2],
+                acc[fc][3] + bias[fc][3]);
     }
   }
   SDDM_STAMP(a, 2);
@@ -415,7 +415,12 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
     const vec8 x = __builtin_bit_cast(vec8, xr[q]);
     float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = in ? silu_fast(to_f32<T>(x[j]) * sc[j] + sh[j]) : 0.f;
+    for (int j = 0; j < 8; j += 2) {
+      const f32x2 o = silu2(f32x2{to_f32<T>(x[j]), to_f32<T>(x[j + 1])} * f32x2{sc[j], sc[j + 1]} +
+                            f32x2{sh[j], sh[j + 1]});
+      v[j] = in ? o.x : 0.f;
+      v[j + 1] = in ? o.y : 0.f;
+    }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if constexpr (sizeof(T) == 4) {
       const Frag<float> A{f32x4{wv[0], wv[1], wv[2], wv[3]}, f32x4{wv[4], wv[5], wv[6], wv[7]}};
