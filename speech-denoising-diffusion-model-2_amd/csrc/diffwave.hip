@@ -1,0 +1,398 @@
+// DiffWave denoiser (reference model/diffwave.py) for SDDM_spectrogram.infer (model.py:212-257).
+//
+// Activations are sample-major [B][N][C] in the compute dtype T, so one sample's channels are
+// contiguous 16-byte units and every MFMA operand fragment is one vector load.  Per sampling
+// call the step-invariant work runs once: the SpectrogramUpsampler (2 ConvTranspose2d passes,
+// diffwave.py:48-61) and the conditioner projections of all residual layers
+// (conditioner_projection, diffwave.py:93), kept as cond[B][N][L][2C]; the noise-step
+// embedding MLP and every layer's diffusion_projection are tabulated for all t (one row per t).
+// Per reverse step: input projection, one fused kernel per residual layer, one output kernel.
+//
+// Fused residual layer (diffwave.py:90-108), one block = 128 samples of one clip, 4 waves:
+//   1. stage y = x + diffusion_projection at the 3 dilated taps (n - d, n, n + d; zero outside
+//      the clip: Conv1d zero padding applies to y) into a plane-major LDS image;
+//   2. dilated_conv as an MFMA GEMM (K = 3 x 64): wave w owns gate rows [16w, 16w+16) and the
+//      matching filter rows [64+16w, ...), so sigmoid(gate) * tanh(filter) pairs sit in the same
+//      lane; + bias + conditioner;
+//   3. the gated activation goes back to LDS (plane-major) and output_residual / output_projection
+//      run as one K = 64 GEMM; the epilogue writes (x + residual) / sqrt(2) to the other x buffer
+//      and accumulates the skip sum in fp32.
+#include "conv_common.h"
+#include "kernels.h"
+
+namespace sddm {
+
+constexpr int DW_C = 64;            // residual_channels (the kernels are built for 64)
+constexpr int DW_MS = 128;          // samples per layer block
+
+__device__ __forceinline__ float dw_silu(float x) { return x * (1.0f / (1.0f + expf(-x))); }
+__device__ __forceinline__ float dw_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---------------- noise-step embedding + diffusion projections of every layer ----------------
+__global__ __launch_bounds__(512) void dw_embed_kernel(DWEmbedArgs a) {
+  __shared__ float enc[128], h1[512], h2[512];
+  const int r = blockIdx.x, tid = threadIdx.x;
+  const float nl = a.noise_levels ? a.noise_levels[r] : (a.time_step_mode ? (float)r : a.table[r]);
+  if (tid < 64) {                                   // diffwave.py:41-45
+    const float v = nl * a.emb_vec[tid];
+    enc[tid] = sinf(v);
+    enc[tid + 64] = cosf(v);
+  }
+  __syncthreads();
+  {
+    float s = a.b1[tid];
+    for (int k = 0; k < 128; ++k) s += a.w1[tid * 128 + k] * enc[k];
+    h1[tid] = dw_silu(s);
+  }
+  __syncthreads();
+  {
+    float s = a.b2[tid];
+    for (int k = 0; k < 512; ++k) s += a.w2[tid * 512 + k] * h1[k];
+    h2[tid] = dw_silu(s);
+  }
+  __syncthreads();
+  for (int o = tid; o < a.L * DW_C; o += 512) {    // diffusion_projection of every layer
+    float s = a.pb[o];
+    const float* w = a.pw + (size_t)o * 512;
+    for (int k = 0; k < 512; ++k) s += w[k] * h2[k];
+    a.out[(size_t)r * a.L * DW_C + o] = s;
+  }
+}
+
+hipError_t launch_dw_embed(const DWEmbedArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(dw_embed_kernel, dim3(a.R), dim3(512), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- SpectrogramUpsampler (ConvTranspose2d [3,32] stride [1,16] pad [1,8]) ----------------
+// out(h, w) = bias + sum_{kh, kw} in(h + 1 - kh, (w + 8 - kw) / 16) k(kh, kw) over the kw with
+// (w + 8 - kw) % 16 == 0, then leaky_relu(0.4)
+__device__ __forceinline__ float dw_up_point(const float* in, int H, int Win, const float* k, float bias, int h, int w) {
+  float s = bias;
+  const int kw0 = (w + 8) & 15;
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+    const int hi = h + 1 - kh;
+    if (hi < 0 || hi >= H) continue;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int kw = kw0 + 16 * m;
+      const int wi = (w + 8 - kw) >> 4;
+      if (wi < 0 || wi >= Win) continue;
+      s += in[hi * Win + wi] * k[kh * 32 + kw];
+    }
+  }
+  return s > 0.f ? s : s * 0.4f;
+}
+
+__global__ __launch_bounds__(256) void dw_upsample1_kernel(DWUpArgs a) {
+  const int Wo = 16 * a.F;
+  const int64_t total = (int64_t)a.B * a.H * Wo;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int w = (int)(i % Wo);
+    const int64_t bh = i / Wo;
+    const int h = (int)(bh % a.H), b = (int)(bh / a.H);
+    a.mid[i] = dw_up_point(a.spec + (size_t)b * a.H * a.F, a.H, a.F, a.k1, a.b1[0], h, w);
+  }
+}
+
+// second pass, written sample-major [B][N][Kp] in T (zero rows h >= H pad K to a multiple of 32)
+template <typename T>
+__global__ __launch_bounds__(256) void dw_upsample2_kernel(DWUpArgs a) {
+  const int Wm = 16 * a.F, N = 256 * a.F;
+  const int64_t total = (int64_t)a.B * N * a.Kp;
+  T* out = (T*)a.out;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int h = (int)(i % a.Kp);
+    const int64_t bn = i / a.Kp;
+    const int n = (int)(bn % N), b = (int)(bn / N);
+    const float v = h < a.H ? dw_up_point(a.mid + (size_t)b * a.H * Wm, a.H, Wm, a.k2, a.b2[0], h, n) : 0.f;
+    out[i] = from_f32<T>(v);
+  }
+}
+
+hipError_t launch_dw_upsample(int dtype, const DWUpArgs& a, hipStream_t s) {
+  const int64_t t1 = (int64_t)a.B * a.H * 16 * a.F, t2 = (int64_t)a.B * 256 * a.F * a.Kp;
+  hipLaunchKernelGGL(dw_upsample1_kernel, dim3((unsigned)std::min<int64_t>((t1 + 255) / 256, 65535)), dim3(256), 0, s, a);
+  const dim3 g2((unsigned)std::min<int64_t>((t2 + 255) / 256, 65535));
+  if (dtype == DT_F32) hipLaunchKernelGGL(dw_upsample2_kernel<float>, g2, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_upsample2_kernel<bf16_t>, g2, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dw_upsample2_kernel<f16_t>, g2, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- conditioner projections of all layers (step-invariant GEMM) ----------------
+// cond[b][n][l][co] = sum_k Wc[l][co][k] spec[b][n][k] + bc[l][co]; block = 128 samples x 128 co
+template <typename T>
+__global__ __launch_bounds__(256) void dw_cond_kernel(DWCondArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int n0 = blockIdx.x * DW_MS, b = blockIdx.y, l = blockIdx.z;
+  const T* W = (const T*)a.w + (size_t)l * 128 * a.Kp;
+  const T* S = (const T*)a.spec + (size_t)b * a.N * a.Kp;
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const T* arow[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) arow[c] = W + (size_t)((wave * 2 + c) * 16 + (lane & 15)) * a.Kp + g * 8;
+  const T* brow[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) brow[p] = S + (size_t)min(n0 + p * 16 + (lane & 15), a.N - 1) * a.Kp + g * 8;
+  for (int k = 0; k < a.Kp; k += 32) {
+    Frag<T> af[2], bf[8];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) af[c] = load_frag<T>((const char*)(arow[c] + k));
+#pragma unroll
+    for (int p = 0; p < 8; ++p) bf[p] = load_frag<T>((const char*)(brow[p] + k));
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int p = 0; p < 8; ++p) mfma_frag(acc[c][p], af[c], bf[p]);
+  }
+  T* out = (T*)a.out;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int co = (wave * 2 + c) * 16 + 4 * g;
+    float bias[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[i] = a.bias[l * 128 + co + i];
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int n = n0 + p * 16 + (lane & 15);
+      if (n >= a.N) continue;
+      store4<T>(out + (((size_t)b * a.N + n) * a.L + l) * 128 + co, acc[c][p][0] + bias[0], acc[c][p][1] + bias[1],
+                acc[c][p][2] + bias[2], acc[c][p][3] + bias[3]);
+    }
+  }
+}
+
+hipError_t launch_dw_cond(int dtype, const DWCondArgs& a, hipStream_t s) {
+  if (a.Kp % 32) return hipErrorInvalidValue;
+  const dim3 grid((a.N + DW_MS - 1) / DW_MS, a.B, a.L);
+  if (dtype == DT_F32) hipLaunchKernelGGL(dw_cond_kernel<float>, grid, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_cond_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dw_cond_kernel<f16_t>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- input projection (diffwave.py:146-147) ----------------
+template <typename T>
+__global__ __launch_bounds__(256) void dw_input_kernel(DWInArgs a) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(VE)));
+  const int64_t total = a.total * (DW_C / VE);
+  if (a.t_dev && blockIdx.x == 0 && threadIdx.x == 0) *a.t_dev -= 1;   // this step's t
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int q = (int)(i % (DW_C / VE));
+    const float au = a.audio[i / (DW_C / VE)];
+    vec v;
+#pragma unroll
+    for (int e = 0; e < VE; ++e) v[e] = from_f32<T>(fmaxf(a.w[q * VE + e] * au + a.b[q * VE + e], 0.f));
+    *(vec*)((T*)a.x + i * VE) = v;
+  }
+}
+
+hipError_t launch_dw_input(int dtype, const DWInArgs& a, hipStream_t s) {
+  const dim3 grid((unsigned)std::min<int64_t>((a.total * 8 + 255) / 256, 8192));
+  if (dtype == DT_F32) hipLaunchKernelGGL(dw_input_kernel<float>, grid, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_input_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dw_input_kernel<f16_t>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- fused residual layer ----------------
+template <typename T>
+__global__ __launch_bounds__(256) void dw_layer_kernel(DWLayerArgs a) {
+  constexpr int ES = (int)sizeof(T), VE = 16 / ES;
+  constexpr int UPS = DW_C / VE;                  // 16-byte units (planes) per sample and tap
+  constexpr int PB = 64 / UPS;                    // samples per 64-unit staging group
+  constexpr int PLANE = DW_MS * 16;               // bytes per plane (2 KB, = 0 mod 256)
+  constexpr int NU = 3 * DW_MS * UPS;             // staged units
+  constexpr int MAXU = 12;
+  typedef T vec4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* yin = smem;                               // [3 taps][UPS][128 samples][16 B]
+  char* zl = smem + 3 * UPS * PLANE;              // [UPS][128 samples][16 B]
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int n0 = blockIdx.x * DW_MS, b = blockIdx.y, N = a.N, d = a.dil;
+  const T* xin = (const T*)a.x_in + (size_t)b * N * DW_C;
+  const int row = a.ds_per_b ? b : (a.t_dev ? *a.t_dev : 0);
+  const float* ds = a.ds + ((size_t)row * a.L + a.layer) * DW_C;
+
+  // conditioner + bias of this lane's gate / filter rows (issued first, used after the GEMM)
+  const int cg = wave * 16 + 4 * g;               // gate row base; filter rows cg + 64
+  vec4 cnd[2][8];
+  {
+    const T* cb = (const T*)a.cond + a.layer * 128;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int n = min(n0 + p * 16 + (lane & 15), N - 1);
+      const T* cp = cb + ((size_t)b * N + n) * a.L * 128;
+      cnd[0][p] = *(const vec4*)(cp + cg);
+      cnd[1][p] = *(const vec4*)(cp + cg + 64);
+    }
+  }
+  // ---- 1. y = x + diffusion projection at the three taps -> LDS ----
+  for (int u0 = 0; u0 < NU; u0 += MAXU * 256) {
+    f32x4 reg[MAXU];
+    int dst[MAXU], qv[MAXU];
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      const int u = min(u0 + tid + k * 256, NU - 1);
+      const int tap = u / (DW_MS * UPS), r = u - tap * (DW_MS * UPS);
+      const int grp = r >> 6, j = r & 63, q = j / PB, s = grp * PB + (j % PB);
+      const int n = n0 + s + (tap - 1) * d;
+      const bool ok = n >= 0 && n < N && u0 + tid + k * 256 < NU;
+      reg[k] = *(const f32x4*)(xin + (size_t)min(max(n, 0), N - 1) * DW_C + q * VE);
+      dst[k] = (u0 + tid + k * 256 < NU) ? ((tap * UPS + q) * PLANE + s * 16) : -1;
+      qv[k] = ok ? q : -1;
+    }
+#pragma unroll
+    for (int k = 0; k < MAXU; ++k) {
+      if (dst[k] < 0) continue;
+      typedef T vec __attribute__((ext_vector_type(VE)));
+      vec v = __builtin_bit_cast(vec, reg[k]);
+      const int q = qv[k];
+#pragma unroll
+      for (int e = 0; e < VE; ++e) v[e] = q >= 0 ? from_f32<T>(to_f32<T>(v[e]) + ds[q * VE + e]) : from_f32<T>(0.f);
+      *(f32x4*)(yin + dst[k]) = __builtin_bit_cast(f32x4, v);
+    }
+  }
+  __syncthreads();
+  // ---- 2. dilated conv GEMM: rows {16w.., 64+16w..} x 128 samples, K = 192 ----
+  f32x4 acc[2][8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const T* w1 = (const T*)a.w1;
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int tap = s >> 1, half = s & 1;
+    Frag<T> af[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      af[c] = load_frag<T>((const char*)(w1 + (size_t)(c * 64 + wave * 16 + (lane & 15)) * 192 + s * 32 + g * 8));
+    const char* pb = yin + (tap * UPS + (half * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const Frag<T> bf = load_planes<T>(pb + p * 256, PLANE);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], af[c], bf);
+    }
+  }
+  // ---- gated activation z = sigmoid(gate) * tanh(filter) -> LDS (plane-major) ----
+  {
+    float bg[4], bfl[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { bg[i] = a.b1[cg + i]; bfl[i] = a.b1[cg + 64 + i]; }
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      float z[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gate = acc[0][p][i] + bg[i] + to_f32<T>(cnd[0][p][i]);
+        const float filt = acc[1][p][i] + bfl[i] + to_f32<T>(cnd[1][p][i]);
+        z[i] = dw_sigmoid(gate) * tanhf(filt);
+      }
+      char* zp = zl + (cg / VE) * PLANE + (p * 16 + (lane & 15)) * 16 + (cg % VE) * ES;
+      store4<T>((T*)zp, z[0], z[1], z[2], z[3]);
+    }
+  }
+  __syncthreads();
+  // ---- 3. output_residual / output_projection GEMM: rows {16w.. residual, 64+16w.. skip}, K = 64 ----
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int p = 0; p < 8; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const T* w2 = (const T*)a.w2;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    Frag<T> af[2];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      af[c] = load_frag<T>((const char*)(w2 + (size_t)(c * 64 + wave * 16 + (lane & 15)) * DW_C + s * 32 + g * 8));
+    const char* pb = zl + ((s * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const Frag<T> bf = load_planes<T>(pb + p * 256, PLANE);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], af[c], bf);
+    }
+  }
+  // ---- epilogue: x_out = (x + residual) / sqrt(2), skip (+)= skip ----
+  {
+    const float r2 = 1.41421353816986083984375f;   // (float)sqrt(2.0) (diffwave.py:108)
+    float br[4], bs[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { br[i] = a.b2[cg + i]; bs[i] = a.b2[64 + cg + i]; }
+    T* xo = (T*)a.x_out + (size_t)b * N * DW_C;
+    float* sk = a.skip + (size_t)b * N * DW_C;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int n = n0 + p * 16 + (lane & 15);
+      if (n >= N) continue;
+      const vec4 xv = *(const vec4*)(xin + (size_t)n * DW_C + cg);
+      store4<T>(xo + (size_t)n * DW_C + cg, (to_f32<T>(xv[0]) + (acc[0][p][0] + br[0])) / r2,
+                (to_f32<T>(xv[1]) + (acc[0][p][1] + br[1])) / r2, (to_f32<T>(xv[2]) + (acc[0][p][2] + br[2])) / r2,
+                (to_f32<T>(xv[3]) + (acc[0][p][3] + br[3])) / r2);
+      f32x4* sp = (f32x4*)(sk + (size_t)n * DW_C + cg);
+      f32x4 v = f32x4{acc[1][p][0] + bs[0], acc[1][p][1] + bs[1], acc[1][p][2] + bs[2], acc[1][p][3] + bs[3]};
+      if (!a.first) v = *sp + v;
+      *sp = v;
+    }
+  }
+}
+
+size_t dw_layer_lds_bytes(int dtype) {
+  const int ups = DW_C * (dtype == DT_F32 ? 4 : 2) / 16;
+  return (size_t)4 * ups * DW_MS * 16;
+}
+
+hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
+  const dim3 grid((a.N + DW_MS - 1) / DW_MS, a.B);
+  const size_t lds = dw_layer_lds_bytes(dtype);
+  if (dtype == DT_F32) hipLaunchKernelGGL(dw_layer_kernel<float>, grid, dim3(256), lds, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_layer_kernel<bf16_t>, grid, dim3(256), lds, s, a);
+  else hipLaunchKernelGGL(dw_layer_kernel<f16_t>, grid, dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- output: skip sum / sqrt(L) -> skip_projection -> relu -> output_projection ----------------
+__global__ __launch_bounds__(256) void dw_output_kernel(DWOutArgs a) {
+  __shared__ float wsp[DW_C * DW_C], bsp[DW_C], wop[DW_C];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < DW_C * DW_C; i += 256) wsp[i] = a.wsp[i];
+  if (tid < DW_C) { bsp[tid] = a.bsp[tid]; wop[tid] = a.wop[tid]; }
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * 256 + tid;
+  if (i >= a.total) return;
+  const float rl = a.sqrt_layers;
+  float s[DW_C];
+  const f32x4* sp = (const f32x4*)(a.skip + i * DW_C);
+#pragma unroll
+  for (int q = 0; q < DW_C / 4; ++q) {
+    const f32x4 v = sp[q];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) s[q * 4 + e] = v[e] / rl;
+  }
+  float out = a.bop[0];
+  for (int o = 0; o < DW_C; ++o) {
+    float h = bsp[o];
+#pragma unroll
+    for (int c = 0; c < DW_C; ++c) h += wsp[o * DW_C + c] * s[c];
+    out += wop[o] * fmaxf(h, 0.f);
+  }
+  a.eps[i] = out;
+}
+
+hipError_t launch_dw_output(const DWOutArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(dw_output_kernel, dim3((unsigned)((a.total + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace sddm

@@ -124,4 +124,41 @@ struct InitArgs {
 hipError_t launch_init_state(const InitArgs& a, hipStream_t s);
 hipError_t launch_set_int(int* p, int v, hipStream_t s);
 
+// ---- DiffWave (reference model/diffwave.py; diffwave.hip) ----
+struct DWEmbedArgs {          // DiffusionEmbedding + every layer's diffusion_projection, rows r = 0..R-1
+  const float* noise_levels;  // [R] explicit, or null -> time_step (r) / table[r]
+  const float* table; int time_step_mode; int R;
+  const float* emb_vec;       // [64]
+  const float* w1; const float* b1; const float* w2; const float* b2;   // 128->512, 512->512
+  const float* pw; const float* pb; int L;                               // [L*64][512], [L*64]
+  float* out;                 // [R][L][64]
+};
+hipError_t launch_dw_embed(const DWEmbedArgs& a, hipStream_t s);
+struct DWUpArgs {             // SpectrogramUpsampler: spec [B][H][F] -> out [B][256F][Kp] (T)
+  const float* spec; float* mid; void* out; int B, H, F, Kp;
+  const float* k1; const float* b1; const float* k2; const float* b2;
+};
+hipError_t launch_dw_upsample(int dtype, const DWUpArgs& a, hipStream_t s);
+struct DWCondArgs {           // cond[b][n][l][128] = Wc[l] spec[b][n] + bc[l]
+  const void* spec; const void* w; const float* bias; void* out; int B, N, L, Kp;
+};
+hipError_t launch_dw_cond(int dtype, const DWCondArgs& a, hipStream_t s);
+struct DWInArgs { const float* audio; const float* w; const float* b; void* x; int64_t total; int* t_dev; };
+hipError_t launch_dw_input(int dtype, const DWInArgs& a, hipStream_t s);
+struct DWLayerArgs {
+  const void* x_in; void* x_out; float* skip; int first;
+  const void* cond; int layer, L;
+  const float* ds; const int* t_dev; int ds_per_b;   // [rows][L][64]
+  const void* w1; const float* b1;                   // dilated conv [128][3*64] (k = tap*64 + ci), bias [128]
+  const void* w2; const float* b2;                   // [output_residual; output_projection] [128][64], [128]
+  int dil, N, B;
+};
+hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s);
+size_t dw_layer_lds_bytes(int dtype);
+struct DWOutArgs {
+  const float* skip; const float* wsp; const float* bsp; const float* wop; const float* bop;
+  float sqrt_layers; float* eps; int64_t total;
+};
+hipError_t launch_dw_output(const DWOutArgs& a, hipStream_t s);
+
 }  // namespace sddm

@@ -239,6 +239,8 @@ struct Lane {                         // one row block of the batch: plan + acti
   }
 };
 
+struct DWState;                       // DiffWave path (dw_runtime.h)
+
 struct sddm_ctx {
   int device = 0, dtype = DT_BF16;
   bool configured = false;
@@ -278,6 +280,9 @@ struct sddm_ctx {
   std::vector<int> ev_op;                     // op index of each timed launch
   std::vector<double> ev_bytes, ev_flops;
   std::map<int, ProfAcc> prof_acc;
+  // SDDM_spectrogram + DiffWave
+  std::shared_ptr<DWState> dws;
+  int hop_samples = 256;
 
   const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
   TransCoef coef() const {
@@ -409,6 +414,8 @@ static int upload_tables(sddm_ctx* c) {
   c->tables_dirty = false;
   return SDDM_OK;
 }
+
+#include "dw_runtime.h"
 
 // ---------------------------------------------------------------------------------------------
 // plan: the launch sequence of one UNetModified2 step for batch B
@@ -801,7 +808,7 @@ static int ensure_ready(sddm_ctx* c) {
   for (const auto& kv : c->params)
     if (!kv.second.loaded) FAIL(SDDM_ERR_STATE, "parameter %s not loaded", kv.first.c_str());
   if (c->params_dirty) {
-    const int r = upload_weights(c);
+    const int r = c->dws ? dw_upload_weights(c) : upload_weights(c);
     if (r) return r;
   }
   if (c->tables_dirty) {
@@ -868,6 +875,7 @@ void sddm_destroy(sddm_ctx* c) {
     if (c->ev_done[k]) (void)hipEventDestroy(c->ev_done[k]);
   }
   c->lanes.clear();
+  if (c->dws) c->dws->act.reset();
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->warena.reset();
@@ -908,8 +916,12 @@ int sddm_configure(sddm_ctx* c, const char* json) {
     else FAIL(SDDM_ERR_NOT_IMPLEMENTED, "p_transition '%s' (model.py:20-23)", pt.c_str());
     if (qt != "original" && qt != "conditional") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "q_transition '%s'", qt.c_str());
     c->p_transition = pt;
-  } else if (c->arch_type == "SDDM_spectrogram") {
-    FAIL(SDDM_ERR_NOT_IMPLEMENTED, "arch SDDM_spectrogram (DiffWave/WaveGrad path) is not built in this library version");
+  } else if (c->arch_type == "SDDM_spectrogram") {              // model.py:206-257
+    c->tr_mode = SDDM_TR_ORIGINAL;
+    c->init_mode = 0;
+    c->p_transition = "original";
+    c->hop_samples = (int)aa.number("hop_samples", 256);          // SURVEY Q6 default
+    if (c->hop_samples < 1) FAIL(SDDM_ERR_INVALID_ARG, "hop_samples %d", c->hop_samples);
   } else {
     FAIL(SDDM_ERR_NOT_IMPLEMENTED, "arch type '%s'", c->arch_type.c_str());
   }
@@ -934,7 +946,41 @@ int sddm_configure(sddm_ctx* c, const char* json) {
     c->configured = true;
     return SDDM_OK;
   }
+  if (c->net_type == "DiffWave") {                               // diffwave.py:113-131
+    if (c->arch_type != "SDDM_spectrogram") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "DiffWave needs arch SDDM_spectrogram");
+    const Json& na = net.at("args");
+    auto d = std::make_shared<DWState>();
+    d->C = (int)na.number("residual_channels", 64);
+    d->L = (int)na.number("residual_layers", 30);
+    d->cycle = (int)na.number("dilation_cycle_length", 10);
+    d->bins = (int)na.number("freq_bins", na.number("stft_bins", na.number("n_mels", 513)));
+    d->hop = c->hop_samples;
+    d->Kp = (d->bins + 31) / 32 * 32;
+    if (d->C != 64) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "DiffWave residual_channels %d (kernels are built for 64)", d->C);
+    if (d->L < 1 || d->cycle < 1 || d->bins < 1) FAIL(SDDM_ERR_INVALID_ARG, "DiffWave geometry");
+    if (d->hop != 256) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "hop_samples %d: SpectrogramUpsampler upsamples x256", d->hop);
+    c->T = T;
+    c->tables.swap(tabs);
+    c->tables_dirty = true;
+    c->num_samples = -1;
+    c->params.clear();
+    for (const auto& kv : dw_param_shapes(*d)) {
+      Param p;
+      p.shape = kv.second;
+      c->params[kv.first] = p;
+    }
+    c->params["diffusion_embedding.embedding_vector"].loaded = true;   // optional (default computed)
+    c->dws = d;
+    c->params_dirty = true;
+    c->plan_B = -1;
+    c->lanes.clear();
+    c->warena.reset();
+    c->configured = true;
+    return SDDM_OK;
+  }
   if (c->net_type != "UNetModified2") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "network type '%s'", c->net_type.c_str());
+  if (c->arch_type != "SDDM") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "UNetModified2 under arch '%s'", c->arch_type.c_str());
+  c->dws.reset();
   const Json& na = net.at("args");
   UNetCfg u;
   u.in_channel = (int)na.number("in_channel", 2);
@@ -1059,6 +1105,7 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
   int r = ensure_ready(c);
   if (r) return r;
   if (!cond || !out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  if (c->dws) return dw_sample(c, cond, B, N, seed, row_offset, out, record, sample_inter, (hipStream_t)stream);
   r = prepare_plan(c, B, N);
   if (r) return r;
   hipStream_t user = (hipStream_t)stream;
@@ -1159,6 +1206,7 @@ int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const
   int r = ensure_ready(c);
   if (r) return r;
   if (!cond || !x_t || !noise_level || !eps_out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  if (c->dws) return dw_forward(c, cond, x_t, noise_level, B, N, eps_out, (hipStream_t)stream);
   r = prepare_plan(c, B, N);
   if (r) return r;
   hipStream_t s = (hipStream_t)stream;

@@ -42,15 +42,21 @@ class SDDM(nn.Module):
 
     def library_config(self):
         net = self.noise_estimate_model
-        return {"arch": {"type": type(self).__name__,
-                         "args": {"noise_condition": self.noise_condition, "p_transition": self.p_transition,
-                                  "q_transition": self.q_transition}},
+        args = {"noise_condition": self.noise_condition, "p_transition": self.p_transition,
+                "q_transition": self.q_transition}
+        if hasattr(self, "hop_samples"):
+            args = {"noise_condition": self.noise_condition, "hop_samples": self.hop_samples}
+        return {"arch": {"type": type(self).__name__, "args": args},
                 "diffusion": {"type": "GaussianDiffusion", "args": self.diffusion.schedule_args},
                 "network": {"type": type(net).__name__, "args": net.config_args},
                 "num_samples": getattr(net, "num_samples", -1)}
 
     def _context(self, device):
-        sd = self.state_dict()
+        sd = dict(self.state_dict())
+        net = self.noise_estimate_model
+        if hasattr(net, "library_params"):       # plain attributes the library needs (DiffWave)
+            for k, v in net.library_params().items():
+                sd.setdefault("noise_estimate_model." + k, v)
         key = (device.index or 0, self.compute_dtype) + tuple((k, v.data_ptr(), v._version) for k, v in sd.items())
         if self._ctx is None or self._ctx_key != key:
             ctx = sddm_hip.Context(self.library_config(), device.index or 0, self.compute_dtype)
@@ -91,5 +97,21 @@ class SDDM_spectrogram(SDDM):
 
     @torch.no_grad()
     def infer(self, condition, continuous=False, seed=None, row_offset=0):
-        raise NotImplementedError("SDDM_spectrogram (DiffWave / WaveGrad) sampling is not in this library "
-                                  "version; see DESIGN.md §Scope")
+        """Reverse diffusion from x_T = randn(B, 1, hop * F) (model.py:212-257).
+        condition: spectrogram [B, bins, F] on the HIP device -> [B, 1, hop * F]."""
+        if not condition.is_cuda:
+            raise RuntimeError("SDDM_spectrogram.infer runs on the HIP device; move the condition to cuda")
+        spec = condition.contiguous().float()
+        ctx = self._context(spec.device)
+        seed = _seed_from_torch() if seed is None else int(seed)
+        B = spec.shape[0]
+        out = torch.empty((B, 1, self.hop_samples * spec.shape[-1]), dtype=torch.float32, device=spec.device)
+        if not continuous:
+            ctx.sample(spec, out, seed, row_offset)
+            return out
+        assert B == 1, "Batch size must be 1 to do continuous sampling"             # model.py:224
+        inter = 1 | (self.num_timesteps // 100)
+        nrec = self.num_timesteps // inter
+        record = torch.empty((max(nrec, 1),) + tuple(out.shape), dtype=torch.float32, device=spec.device)
+        ctx.sample_continuous(spec, out, record, inter, seed, row_offset)
+        return [condition] + [record[i] for i in range(nrec)]

@@ -141,20 +141,20 @@ class Context:
     # the torch tensors below are device tensors (fp32, contiguous) on self.device
     def sample(self, cond, out, seed, row_offset=0):
         import torch
-        B, N = cond.shape[0], cond.shape[-1]
+        B, N = out.shape[0], out.shape[-1]          # spectrogram archs: cond is [B, bins, frames]
         check(lib().sddm_sample(self._h, _ptr(cond), B, N, int(seed) & (2 ** 64 - 1), int(row_offset),
                                 _ptr(out), _stream(torch, cond.device)))
 
     def sample_continuous(self, cond, out, record, sample_inter, seed, row_offset=0):
         import torch
-        B, N = cond.shape[0], cond.shape[-1]
+        B, N = out.shape[0], out.shape[-1]
         check(lib().sddm_sample_continuous(self._h, _ptr(cond), B, N, int(seed) & (2 ** 64 - 1),
                                            int(row_offset), _ptr(out), _ptr(record), int(sample_inter),
                                            _stream(torch, cond.device)))
 
     def network_forward(self, cond, x_t, noise_level, eps_out):
         import torch
-        B, N = cond.shape[0], cond.shape[-1]
+        B, N = x_t.shape[0], x_t.shape[-1]
         check(lib().sddm_network_forward(self._h, _ptr(cond), _ptr(x_t), _ptr(noise_level), B, N,
                                          _ptr(eps_out), _stream(torch, cond.device)))
 

@@ -57,3 +57,9 @@ def rms(a, b):
     a = np.asarray(a, np.float64)
     b = np.asarray(b, np.float64)
     return float(np.sqrt(np.mean((a - b) ** 2)))
+
+
+def diffwave_params(seed=0, bins=513):
+    """Deterministic DiffWave weights with the reference key names (no module prefix)."""
+    from oracle.diffwave import param_shapes
+    return make_params(param_shapes(bins), seed)

@@ -187,6 +187,57 @@ def main():
         if N <= 2112:
             inf[key + "/steps"] = np.stack(steps)
     np.savez_compressed(os.path.join(args.out, "unet_infer.npz"), **inf)
+
+    # 7. DiffWave (model/diffwave.py) forward and SDDM_spectrogram.infer (model.py:212-257)
+    #    config_diffwave.json network args; spectrogram [B, 513, F] ~ U[0, 1]
+    from model.diffwave import DiffWave, DiffusionEmbedding
+    from model.model import SDDM_spectrogram
+    emb["diffwave_embedding_vector"] = DiffusionEmbedding().embedding_vector.numpy().copy()
+    dw = {}
+    rng = np.random.default_rng(5)
+    for F, B in ((6, 2),):
+        net = DiffWave(num_samples=-1, num_timesteps=3, freq_bins=513, residual_channels=64,
+                       residual_layers=30, dilation_cycle_length=10)
+        shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+        P = make_params(shapes, 0)
+        net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+        net.eval()
+        spec = rng.uniform(0, 1, (B, 513, F)).astype(np.float32)
+        N = 256 * F
+        audio = philox.normal(13, 0, (B, 1, N))
+        steps = np.array([3.0, 1.0][:B], dtype=np.float32).reshape(B, 1, 1)
+        with torch.no_grad():
+            y = net(torch.from_numpy(spec), torch.from_numpy(audio), torch.from_numpy(steps))
+            up = net.spectrogram_upsampler(torch.from_numpy(spec))
+        key = f"dw/fw/{F}x{B}"
+        dw[key + "/spec"], dw[key + "/audio"], dw[key + "/step"] = spec, audio, steps.reshape(-1)
+        dw[key + "/eps"] = y.numpy().copy()
+        dw[key + "/upsampled"] = up.numpy()[:, :64].copy()   # first 64 bins (fixture size)
+        # full sampling loop, time_step conditioning (config_diffwave.json arch args)
+        sched = SCHEDULES[10]
+        d = GaussianDiffusion(*sched, device="cpu")
+        m = SDDM_spectrogram(d, net, hop_samples=256, noise_condition="time_step")
+        m.eval()
+        steps_rec = []
+        orig = d.p_transition
+
+        def rec(*a, **kw):
+            y = orig(*a, **kw)
+            steps_rec.append(y.numpy().copy())
+            return y
+        d.p_transition = rec
+        inj = NoiseInjector(torch, philox, 7)
+        inj.draws = [0] + list(range(sched[1], 1, -1))
+        with inj, torch.no_grad():
+            y = m.infer(torch.from_numpy(spec))
+        key = f"dw/inf/time_step/{sched_key(sched)}/{F}x{B}"
+        dw[key + "/spec"] = spec
+        dw[key + "/out"] = y.numpy().copy()
+        dw[key + "/steps"] = np.stack(steps_rec)
+    keys["diffwave_513"] = [[k, list(v.shape)] for k, v in net.state_dict().items()]
+    with open(os.path.join(args.out, "state_dict_keys.json"), "w") as f:
+        json.dump(keys, f, indent=0)
+    np.savez_compressed(os.path.join(args.out, "diffwave.npz"), **dw)
     np.savez_compressed(os.path.join(args.out, "embedding.npz"), **emb)
     print("wrote fixtures to", args.out)
 

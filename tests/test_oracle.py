@@ -114,3 +114,31 @@ def test_frame_index_and_overlap_add():
     cover = unet.overlap_add(np.ones((1, 1, 32, 128), np.float32), 2112, 64)[0, 0]
     assert cover[:64].tolist() == [1.0] * 64 and cover[-64:].tolist() == [1.0] * 64
     assert (cover[64:-64] == 2.0).all()
+
+
+# ---------------- DiffWave (reference model/diffwave.py) ----------------
+def test_diffwave_oracle_matches_reference_goldens():
+    from oracle import diffwave as dw
+    from _helpers import diffwave_params
+    z = golden("diffwave.npz")
+    e = golden("embedding.npz")["diffwave_embedding_vector"]
+    ulp = np.abs(dw.embedding_vector() - e) / np.spacing(e)
+    assert ulp.max() <= 1.0                     # torch's fp32 pow (SLEEF) vs correctly rounded
+    P = diffwave_params()
+    k = "dw/fw/6x2"
+    assert np.abs(dw.upsample(P, z[f"{k}/spec"])[:, :64] - z[f"{k}/upsampled"]).max() <= 1e-6
+    eps = dw.forward(P, z[f"{k}/spec"], z[f"{k}/audio"], z[f"{k}/step"])
+    assert np.sqrt(np.mean((eps - z[f"{k}/eps"]) ** 2)) <= 1e-6
+
+
+def test_diffwave_oracle_sampling_matches_reference():
+    from oracle import diffwave as dw, sampler
+    from _helpers import diffwave_params, tables_from_golden
+    z = golden("diffwave.npz")
+    P = diffwave_params()
+    sk = "linear_3_0.0001_0.05"
+    k = f"dw/inf/time_step/{sk}/6x2"
+    tab = tables_from_golden(sk)
+    out = sampler.infer_spectrogram(lambda s, x, nl: dw.forward(P, s, x, nl), tab, z[f"{k}/spec"], 256,
+                                    noise_condition="time_step", seed=7)
+    assert np.sqrt(np.mean((out - z[f"{k}/out"]) ** 2)) <= 1e-5
