@@ -63,3 +63,9 @@ def diffwave_params(seed=0, bins=513):
     """Deterministic DiffWave weights with the reference key names (no module prefix)."""
     from oracle.diffwave import param_shapes
     return make_params(param_shapes(bins), seed)
+
+
+def wavegrad_params(seed=0):
+    """Deterministic WaveGrad weights with the reference key names (no module prefix)."""
+    from oracle.wavegrad import param_shapes
+    return make_params(param_shapes(), seed)

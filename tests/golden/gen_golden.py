@@ -66,6 +66,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
     ap.add_argument("--out", default=HERE)
+    ap.add_argument("--only", default=None, help="regenerate one fixture group (wavegrad)")
     args = ap.parse_args()
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "speech-denoising-diffusion-model-2_amd"))
@@ -81,6 +82,9 @@ def main():
     from model.UNetModified2 import UNetModified2, PositionalEncoding
     from model.model import SDDM
     out = {}
+    if args.only == "wavegrad":
+        gen_wavegrad(torch, philox, make_params, GaussianDiffusion, args.out)
+        return
 
     # 1. schedule tables (diffusion.py:50-161)
     for s in SCHEDULES:
@@ -239,7 +243,54 @@ def main():
         json.dump(keys, f, indent=0)
     np.savez_compressed(os.path.join(args.out, "diffwave.npz"), **dw)
     np.savez_compressed(os.path.join(args.out, "embedding.npz"), **emb)
+    gen_wavegrad(torch, philox, make_params, GaussianDiffusion, args.out)
     print("wrote fixtures to", args.out)
+
+
+def gen_wavegrad(torch, philox, make_params, GaussianDiffusion, out_dir):
+    """8. WaveGrad (model/wavegrad.py) forward, and the reverse loop of SDDM_spectrogram.infer
+    (model.py:212-257) with the SURVEY Q4 adapter (x_t [B,1,N] -> audio [B,N], noise level [B],
+    eps reshaped to [B,1,N]): the reference wiring itself fails on WaveGrad's 4-D Conv1d input."""
+    from model.wavegrad import WaveGrad
+    wg = {}
+    rng = np.random.default_rng(9)
+    F, B = 6, 2
+    net = WaveGrad()
+    shapes = {k: tuple(v.shape) for k, v in net.state_dict().items()}
+    P = make_params(shapes, 0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    net.eval()
+    spec = rng.uniform(0, 1, (B, 128, F)).astype(np.float32)
+    N = 300 * F
+    audio = philox.normal(17, 0, (B, N))
+    nl = np.array([0.7, 0.3], dtype=np.float32)
+    with torch.no_grad():
+        y = net(torch.from_numpy(spec), torch.from_numpy(audio), torch.from_numpy(nl))
+    key = f"wg/fw/{F}x{B}"
+    wg[key + "/spec"], wg[key + "/audio"], wg[key + "/noise_level"] = spec, audio, nl
+    wg[key + "/eps"] = y.numpy().copy()
+    sched = ("linear", 3, 1e-4, 0.05)
+    d = GaussianDiffusion(*sched, device="cpu")
+    inj = NoiseInjector(torch, philox, 7)
+    inj.draws = [0] + list(range(sched[1], 1, -1))
+    steps = []
+    with inj, torch.no_grad():
+        x = torch.randn(B, 1, N)                                   # model.py:216
+        for t in reversed(range(1, sched[1] + 1)):
+            noise_level = d.get_noise_level(t) * torch.ones(B)     # model.py:227-229 (adapter: [B])
+            eps = net(torch.from_numpy(spec), x[:, 0, :], noise_level).reshape(B, 1, N)
+            x = d.p_transition(x, t, eps)
+            steps.append(x.numpy().copy())
+    key = f"wg/inf/sqrt_alpha_bar/{sched_key(sched)}/{F}x{B}"
+    wg[key + "/spec"] = spec
+    wg[key + "/out"] = x.numpy().copy()
+    wg[key + "/steps"] = np.stack(steps)
+    np.savez_compressed(os.path.join(out_dir, "wavegrad.npz"), **wg)
+    with open(os.path.join(out_dir, "state_dict_keys.json")) as f:
+        keys = json.load(f)
+    keys["wavegrad"] = [[k, list(v.shape)] for k, v in net.state_dict().items()]
+    with open(os.path.join(out_dir, "state_dict_keys.json"), "w") as f:
+        json.dump(keys, f, indent=0)
 
 
 if __name__ == "__main__":

@@ -142,3 +142,37 @@ def test_diffwave_oracle_sampling_matches_reference():
     out = sampler.infer_spectrogram(lambda s, x, nl: dw.forward(P, s, x, nl), tab, z[f"{k}/spec"], 256,
                                     noise_condition="time_step", seed=7)
     assert np.sqrt(np.mean((out - z[f"{k}/out"]) ** 2)) <= 1e-5
+
+
+# ---------------- WaveGrad (reference model/wavegrad.py) ----------------
+def test_wavegrad_oracle_matches_reference_goldens():
+    from oracle import wavegrad as wg
+    from _helpers import wavegrad_params
+    z = golden("wavegrad.npz")
+    k = "wg/fw/6x2"
+    eps = wg.forward(wavegrad_params(), z[f"{k}/spec"], z[f"{k}/audio"], z[f"{k}/noise_level"])
+    assert eps.shape == z[f"{k}/eps"].shape
+    assert rms(eps, z[f"{k}/eps"]) <= 1e-6
+
+
+def test_wavegrad_param_shapes_match_reference_state_dict():
+    import json
+    import os
+    from oracle import wavegrad as wg
+    here = os.path.join(os.path.dirname(__file__), "golden", "state_dict_keys.json")
+    keys = json.load(open(here))["wavegrad"]
+    assert {k: tuple(s) for k, s in keys} == wg.param_shapes()
+
+
+def test_wavegrad_oracle_sampling_matches_reference():
+    """SDDM_spectrogram loop with the SURVEY Q4 adapter (eps [B,N] -> [B,1,N])."""
+    from oracle import wavegrad as wg
+    from _helpers import wavegrad_params
+    z = golden("wavegrad.npz")
+    P = wavegrad_params()
+    sk = "linear_3_0.0001_0.05"
+    k = f"wg/inf/sqrt_alpha_bar/{sk}/6x2"
+    tab = tables_from_golden(sk)
+    out = sampler.infer_spectrogram(lambda s, x, nl: wg.forward(P, s, x[:, 0], nl)[:, None], tab, z[f"{k}/spec"],
+                                    wg.HOP, noise_condition="sqrt_alpha_bar", seed=7)
+    assert rms(out, z[f"{k}/out"]) <= 1e-5
