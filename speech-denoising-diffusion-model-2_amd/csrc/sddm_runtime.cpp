@@ -240,6 +240,7 @@ struct Lane {                         // one row block of the batch: plan + acti
 };
 
 struct DWState;                       // DiffWave path (dw_runtime.h)
+struct WGState;                       // WaveGrad path (wg_runtime.h)
 
 struct sddm_ctx {
   int device = 0, dtype = DT_BF16;
@@ -282,6 +283,7 @@ struct sddm_ctx {
   std::map<int, ProfAcc> prof_acc;
   // SDDM_spectrogram + DiffWave
   std::shared_ptr<DWState> dws;
+  std::shared_ptr<WGState> wgs;
   int hop_samples = 256;
 
   const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
@@ -416,6 +418,7 @@ static int upload_tables(sddm_ctx* c) {
 }
 
 #include "dw_runtime.h"
+#include "wg_runtime.h"
 
 // ---------------------------------------------------------------------------------------------
 // plan: the launch sequence of one UNetModified2 step for batch B
@@ -808,7 +811,7 @@ static int ensure_ready(sddm_ctx* c) {
   for (const auto& kv : c->params)
     if (!kv.second.loaded) FAIL(SDDM_ERR_STATE, "parameter %s not loaded", kv.first.c_str());
   if (c->params_dirty) {
-    const int r = c->dws ? dw_upload_weights(c) : upload_weights(c);
+    const int r = c->dws ? dw_upload_weights(c) : (c->wgs ? wg_upload_weights(c) : upload_weights(c));
     if (r) return r;
   }
   if (c->tables_dirty) {
@@ -876,6 +879,7 @@ void sddm_destroy(sddm_ctx* c) {
   }
   c->lanes.clear();
   if (c->dws) c->dws->act.reset();
+  if (c->wgs) c->wgs->act.reset();
   if (c->ev_in) (void)hipEventDestroy(c->ev_in);
   for (hipEvent_t e : c->ev_pool) (void)hipEventDestroy(e);
   c->warena.reset();
@@ -971,6 +975,30 @@ int sddm_configure(sddm_ctx* c, const char* json) {
     }
     c->params["diffusion_embedding.embedding_vector"].loaded = true;   // optional (default computed)
     c->dws = d;
+    c->wgs.reset();
+    c->params_dirty = true;
+    c->plan_B = -1;
+    c->lanes.clear();
+    c->warena.reset();
+    c->configured = true;
+    return SDDM_OK;
+  }
+  if (c->net_type == "WaveGrad") {                               // wavegrad.py:140-179
+    if (c->arch_type != "SDDM_spectrogram") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "WaveGrad needs arch SDDM_spectrogram");
+    if (c->hop_samples != WGState::kHop)
+      FAIL(SDDM_ERR_NOT_IMPLEMENTED, "hop_samples %d: WaveGrad upsamples x300 (config_wavegrad.json:8)", c->hop_samples);
+    c->T = T;
+    c->tables.swap(tabs);
+    c->tables_dirty = true;
+    c->num_samples = -1;
+    c->params.clear();
+    for (const auto& kv : wg_param_shapes()) {
+      Param p;
+      p.shape = kv.second;
+      c->params[kv.first] = p;
+    }
+    c->dws.reset();
+    c->wgs = std::make_shared<WGState>();
     c->params_dirty = true;
     c->plan_B = -1;
     c->lanes.clear();
@@ -981,6 +1009,7 @@ int sddm_configure(sddm_ctx* c, const char* json) {
   if (c->net_type != "UNetModified2") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "network type '%s'", c->net_type.c_str());
   if (c->arch_type != "SDDM") FAIL(SDDM_ERR_NOT_IMPLEMENTED, "UNetModified2 under arch '%s'", c->arch_type.c_str());
   c->dws.reset();
+  c->wgs.reset();
   const Json& na = net.at("args");
   UNetCfg u;
   u.in_channel = (int)na.number("in_channel", 2);
@@ -1106,6 +1135,7 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
   if (r) return r;
   if (!cond || !out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
   if (c->dws) return dw_sample(c, cond, B, N, seed, row_offset, out, record, sample_inter, (hipStream_t)stream);
+  if (c->wgs) return wg_sample(c, cond, B, N, seed, row_offset, out, record, sample_inter, (hipStream_t)stream);
   r = prepare_plan(c, B, N);
   if (r) return r;
   hipStream_t user = (hipStream_t)stream;
@@ -1207,6 +1237,7 @@ int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const
   if (r) return r;
   if (!cond || !x_t || !noise_level || !eps_out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
   if (c->dws) return dw_forward(c, cond, x_t, noise_level, B, N, eps_out, (hipStream_t)stream);
+  if (c->wgs) return wg_forward(c, cond, x_t, noise_level, B, N, eps_out, (hipStream_t)stream);
   r = prepare_plan(c, B, N);
   if (r) return r;
   hipStream_t s = (hipStream_t)stream;

@@ -1,0 +1,287 @@
+// WaveGrad denoiser (reference model/wavegrad.py) for SDDM_spectrogram.infer (model.py:212-257).
+//
+// Activations are sample-major [B][T][C] in the compute dtype, so one time position's channels
+// are contiguous and each MFMA operand fragment (8 channels) is one 16-byte (bf16/f16) or two
+// 16-byte (fp32) vector loads.  Every convolution of the network -- DBlock / UBlock dilated convs,
+// the 1x1 residual_dense / block1, FiLM input/output convs, first_conv and last_conv -- is one
+// launch of wg_conv_kernel: an implicit GEMM over K = taps x Cin whose B-operand loader applies
+// the layer's input transform on the fly (nearest up/down interpolation as an index map, the
+// leaky_relu, the FiLM affine shift + scale * x) and whose epilogue fuses bias, the FiLM
+// input_conv's leaky_relu + PositionalEncoding, and the residual adds.  Nothing but conv outputs
+// is ever written to HBM.
+//
+// Block = 4 waves (256 threads) = 64 output channels x 128 time positions; wave w owns output
+// channels [32 (w & 1), +32) x time [64 (w >> 1), +64) as 2 x 4 MFMA 16x16 tiles.
+#include "conv_common.h"
+#include "wg_kernels.h"
+
+namespace sddm {
+
+constexpr int WG_MC = 64;    // output channels per block
+constexpr int WG_MT = 128;   // time positions per block
+
+__device__ __forceinline__ float wg_leaky(float x) { return x > 0.f ? x : x * 0.2f; }
+
+template <typename T> __device__ __forceinline__ void load8(const T* p, float* v);
+template <> __device__ __forceinline__ void load8<float>(const float* p, float* v) {
+  const f32x4 a = *(const f32x4*)p, b = *(const f32x4*)(p + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) { v[j] = a[j]; v[4 + j] = b[j]; }
+}
+template <> __device__ __forceinline__ void load8<bf16_t>(const bf16_t* p, float* v) {
+  const bf16x8 a = *(const bf16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)a[j];
+}
+template <> __device__ __forceinline__ void load8<f16_t>(const f16_t* p, float* v) {
+  const f16x8 a = *(const f16x8*)p;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (float)a[j];
+}
+
+template <typename T> __device__ __forceinline__ Frag<T> pack8(const float* v);
+template <> __device__ __forceinline__ Frag<float> pack8<float>(const float* v) {
+  return {f32x4{v[0], v[1], v[2], v[3]}, f32x4{v[4], v[5], v[6], v[7]}};
+}
+template <> __device__ __forceinline__ Frag<bf16_t> pack8<bf16_t>(const float* v) {
+  bf16x8 a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = (bf16_t)v[j];
+  return {a};
+}
+template <> __device__ __forceinline__ Frag<f16_t> pack8<f16_t>(const float* v) {
+  f16x8 a;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) a[j] = (f16_t)v[j];
+  return {a};
+}
+
+template <typename T> __device__ __forceinline__ Frag<T> zero_frag() {
+  float z[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  return pack8<T>(z);
+}
+
+__device__ __forceinline__ int wg_map(int t, int map, int f) {
+  return map == WG_MAP_UP ? t / f : (map == WG_MAP_DOWN ? t * f : t);
+}
+
+// B fragment at conv-input position tp (already bounds-checked by the caller via ok)
+template <typename T, int PRE>
+__device__ __forceinline__ Frag<T> wg_load_b(const WGConvArgs& a, const T* src_b, const T* film_b, int tp, bool ok,
+                                             int ci) {
+#pragma clang fp contract(off)
+  if (!ok) return zero_frag<T>();
+  const int sr = wg_map(tp, a.map, a.f);
+  const T* p = src_b + (size_t)sr * a.src_C + ci;
+  if (PRE == 0) return load_frag<T>((const char*)p);
+  float v[8];
+  load8<T>(p, v);
+  if (PRE == 2) {            // leaky(shift + scale * x)   (wavegrad.py:98, 104, 107)
+    float sh[8], sc[8];
+    const T* fp = film_b + (size_t)tp * 2 * a.Cin + ci;
+    load8<T>(fp, sh);
+    load8<T>(fp + a.Cin, sc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = wg_leaky(sh[j] + sc[j] * v[j]);
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = wg_leaky(v[j]);
+  }
+  return pack8<T>(v);
+}
+
+template <typename T, int PRE>
+__global__ __launch_bounds__(256) void wg_conv_kernel(WGConvArgs a) {
+#pragma clang fp contract(off)
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.z;
+  const int co0 = blockIdx.y * WG_MC + (wave & 1) * 32;
+  const int tt0 = blockIdx.x * WG_MT + (wave >> 1) * 64;
+  const int Tc = a.Tc, Cin = a.Cin, KC = a.K * Cin, half = (a.K - 1) / 2;
+  const T* src_b = (const T*)a.src + (size_t)b * a.src_T * a.src_C;
+  const T* film_b = PRE == 2 ? (const T*)a.film + (size_t)b * Tc * 2 * Cin : nullptr;
+  const T* wrow[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) wrow[c] = (const T*)a.w + (size_t)(co0 + c * 16 + l16) * KC + g * 8;
+
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  for (int tap = 0; tap < a.K; ++tap) {
+    int tp[4];
+    bool ok[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int t = tt0 + p * 16 + l16;
+      tp[p] = t + (tap - half) * a.dil;
+      ok[p] = t < Tc && tp[p] >= 0 && tp[p] < Tc;
+    }
+    const int kb = tap * Cin;
+    for (int c0 = 0; c0 < Cin; c0 += 32) {
+      Frag<T> af[2], bfr[4];
+#pragma unroll
+      for (int c = 0; c < 2; ++c) af[c] = load_frag<T>((const char*)(wrow[c] + kb + c0));
+#pragma unroll
+      for (int p = 0; p < 4; ++p) bfr[p] = wg_load_b<T, PRE>(a, src_b, film_b, tp[p], ok[p], c0 + g * 8);
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) mfma_frag(acc[c][p], af[c], bfr[p]);
+    }
+  }
+
+  // epilogue: bias, FiLM leaky + encoding, residual, store
+  const float* enc = nullptr;
+  if (a.post == 1) {
+    const int row = a.enc_per_b ? b : *a.t_dev;
+    enc = a.enc + (size_t)row * a.enc_stride + a.enc_off;
+  }
+  const T* res_b = a.res ? (const T*)a.res + (size_t)b * a.res_T * a.Cout : nullptr;
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const int cb = co0 + c * 16 + 4 * g;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int t = tt0 + p * 16 + l16;
+      if (t >= Tc) continue;
+      float v[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int co = cb + i;
+        float x = acc[c][p][i] + (co < a.Cout ? a.bias[co] : 0.f);
+        if (a.post == 1 && co < a.Cout) x = wg_leaky(x) + enc[co];
+        if (res_b && co < a.Cout) x = x + to_f32<T>(res_b[(size_t)wg_map(t, a.res_map, a.res_f) * a.Cout + co]);
+        v[i] = x;
+      }
+      if (a.out_f32) {
+        float* o = (float*)a.out + ((size_t)b * Tc + t) * a.Cout;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (cb + i < a.Cout) o[cb + i] = v[i];
+      } else if ((a.Cout & 3) == 0) {
+        if (cb < a.Cout) store4<T>((T*)a.out + ((size_t)b * Tc + t) * a.Cout + cb, v[0], v[1], v[2], v[3]);
+      } else {
+        T* o = (T*)a.out + ((size_t)b * Tc + t) * a.Cout;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (cb + i < a.Cout) o[cb + i] = from_f32<T>(v[i]);
+      }
+    }
+  }
+}
+
+template <typename T>
+static void wg_conv_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
+  if (a.pre == 0) hipLaunchKernelGGL((wg_conv_kernel<T, 0>), grid, dim3(256), 0, s, a);
+  else if (a.pre == 1) hipLaunchKernelGGL((wg_conv_kernel<T, 1>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((wg_conv_kernel<T, 2>), grid, dim3(256), 0, s, a);
+}
+
+hipError_t launch_wg_conv(int dtype, const WGConvArgs& a, hipStream_t s) {
+  if (a.Cin % 32 || a.Cin > a.src_C || a.K < 1 || a.K % 2 == 0 || a.Tc < 1 || a.B < 1 || a.Cout < 1)
+    return hipErrorInvalidValue;
+  if ((a.map == WG_MAP_UP && (a.f < 1 || a.src_T * a.f != a.Tc)) || (a.map == WG_MAP_DOWN && a.src_T / a.f != a.Tc) ||
+      (a.map == WG_MAP_ID && a.src_T != a.Tc) || (a.pre == 2 && !a.film) || (a.post == 1 && (!a.enc || (!a.enc_per_b && !a.t_dev))))
+    return hipErrorInvalidValue;
+  if (a.res && ((a.res_map == WG_MAP_UP && a.res_T * a.res_f != a.Tc) || (a.res_map == WG_MAP_ID && a.res_T != a.Tc)))
+    return hipErrorInvalidValue;
+  const dim3 grid((a.Tc + WG_MT - 1) / WG_MT, (a.Cout + WG_MC - 1) / WG_MC, a.B);
+  if (dtype == DT_F32) wg_conv_dispatch<float>(a, grid, s);
+  else if (dtype == DT_BF16) wg_conv_dispatch<bf16_t>(a, grid, s);
+  else wg_conv_dispatch<f16_t>(a, grid, s);
+  return hipGetLastError();
+}
+
+// ---------------- downsample.0: Conv1d(1, 32, 5, padding=2) ----------------
+template <typename T>
+__global__ __launch_bounds__(256) void wg_first_kernel(WGFirstArgs a) {
+  __shared__ float w[32 * 5], bias[32];
+  const int tid = threadIdx.x;
+  if (a.t_dev && blockIdx.x == 0 && tid == 0) *a.t_dev -= 1;   // this step's t
+  if (tid < 160) w[tid] = a.w[tid];
+  if (tid < 32) bias[tid] = a.b[tid];
+  __syncthreads();
+  const int64_t total = (int64_t)a.B * a.N;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + tid; i < total; i += (int64_t)gridDim.x * 256) {
+    const int n = (int)(i % a.N);
+    const float* x = a.audio + (i - n);
+    float xv[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int m = n + k - 2;
+      xv[k] = (m >= 0 && m < a.N) ? x[m] : 0.f;
+    }
+    T* o = (T*)a.out + i * 32;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = q * 4 + e;
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s += w[co * 5 + k] * xv[k];
+        v[e] = s + bias[co];
+      }
+      store4<T>(o + q * 4, v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+hipError_t launch_wg_first(int dtype, const WGFirstArgs& a, hipStream_t s) {
+  const int64_t total = (int64_t)a.B * a.N;
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 16384)));
+  if (dtype == DT_F32) hipLaunchKernelGGL(wg_first_kernel<float>, grid, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(wg_first_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(wg_first_kernel<f16_t>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- spectrogram [B][C][F] -> [B][F][C] ----------------
+template <typename T>
+__global__ __launch_bounds__(256) void wg_spec_kernel(WGSpecArgs a) {
+  const int64_t total = (int64_t)a.B * a.F * a.C;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int c = (int)(i % a.C);
+    const int64_t bf = i / a.C;
+    const int f = (int)(bf % a.F), b = (int)(bf / a.F);
+    ((T*)a.out)[i] = from_f32<T>(a.spec[((size_t)b * a.C + c) * a.F + f]);
+  }
+}
+
+hipError_t launch_wg_spec(int dtype, const WGSpecArgs& a, hipStream_t s) {
+  const int64_t total = (int64_t)a.B * a.F * a.C;
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 16384)));
+  if (dtype == DT_F32) hipLaunchKernelGGL(wg_spec_kernel<float>, grid, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(wg_spec_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(wg_spec_kernel<f16_t>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- PositionalEncoding rows (wavegrad.py:44-49) ----------------
+__global__ __launch_bounds__(256) void wg_enc_kernel(WGEncArgs a) {
+#pragma clang fp contract(off)
+  const int r = blockIdx.x;
+  const float nl = a.noise_levels ? a.noise_levels[r] : (a.time_step_mode ? (float)r : a.table[r]);
+  for (int j = threadIdx.x; j < a.n; j += 256) {
+    int i = 0;
+#pragma unroll
+    for (int q = 1; q < 5; ++q)
+      if (j >= a.offs[q]) i = q;
+    const int k = j - a.offs[i], cnt = a.dims[i] / 2;
+    const float e = nl * a.ev[a.offs[i] / 2 + (k % cnt)];
+    a.out[(size_t)r * a.stride + j] = k < cnt ? sinf(e) : cosf(e);
+  }
+}
+
+hipError_t launch_wg_enc(const WGEncArgs& a, hipStream_t s) {
+  if (a.R < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(wg_enc_kernel, dim3(a.R), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace sddm

@@ -25,7 +25,8 @@ if VARIANT:
 else:
     BUILD = os.path.join(HERE, "_build")
     LIB = os.path.join(HERE, "libsddm_hip.so")
-SOURCES = ["kernels.hip", "conv_strip.hip", "conv_deep.hip", "diffwave.hip", "sddm_runtime.cpp", "schedule.cpp"]
+SOURCES = ["kernels.hip", "conv_strip.hip", "conv_deep.hip", "diffwave.hip", "wavegrad.hip", "sddm_runtime.cpp",
+           "schedule.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SDDM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", CSRC, "-I", INCLUDE,
@@ -35,8 +36,18 @@ if VARIANT:
     FLAGS += os.environ.get("SDDM_EXTRA_DEFS", "").split()
 
 
-def _deps():
-    return glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
+def _deps(path, seen=None):
+    """Headers a source includes (transitively), found in csrc/ or include/."""
+    import re
+    seen = set() if seen is None else seen
+    with open(path) as f:
+        for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', f.read(), re.M):
+            for d in (CSRC, INCLUDE):
+                h = os.path.join(d, name)
+                if os.path.exists(h) and h not in seen:
+                    seen.add(h)
+                    _deps(h, seen)
+    return sorted(seen)
 
 
 def _stale(target, inputs):
@@ -48,7 +59,7 @@ def _stale(target, inputs):
 
 def _compile(src):
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if _stale(obj, [os.path.join(CSRC, src)] + _deps()):
+    if _stale(obj, [os.path.join(CSRC, src)] + _deps(os.path.join(CSRC, src))):
         cmd = [HIPCC] + FLAGS + ["-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:

@@ -142,3 +142,27 @@ def test_reference_config_resolves_unchanged(name, tmp_path):
     lib_cfg = model.library_config()
     assert lib_cfg["network"]["args"]["channel_mults"] == [1, 2, 3, 4, 5]
     assert lib_cfg["arch"]["args"]["p_transition"] == "condition_in"
+
+
+def test_wavegrad_facade_state_dict_matches_reference_layout():
+    import model.network as NW
+    ref = json.load(open(os.path.join(GOLDEN, "state_dict_keys.json")))["wavegrad"]
+    sd = NW.WaveGrad().state_dict()
+    assert [[k, list(v.shape)] for k, v in sd.items()] == ref
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference"), reason="reference configs only in the build container")
+def test_reference_wavegrad_config_resolves_unchanged(tmp_path):
+    from parse_config import ConfigParser, read_json
+    import model.diffusion as module_diffusion
+    import model.model as module_arch
+    import model.network as module_network
+    cfg = read_json(os.path.join("/root/reference", "config_wavegrad.json"))
+    cfg["trainer"]["save_dir"] = str(tmp_path)
+    config = ConfigParser(cfg, run_id="w")
+    diffusion = config.init_obj("diffusion", module_diffusion, device="cpu")
+    network = config.init_obj("network", module_network, num_samples=-1)
+    model = config.init_obj("arch", module_arch, diffusion, network)
+    lib_cfg = model.library_config()
+    assert type(model).__name__ == "SDDM_spectrogram" and model.hop_samples == 300
+    assert lib_cfg["network"]["type"] == "WaveGrad" and lib_cfg["diffusion"]["args"]["n_timestep"] == 1000
