@@ -9,6 +9,7 @@ its own B rows (row_offset = rank * B, so results equal a single-GPU run of all 
 outputs are all-gathered over RCCL at the end of the step (weak scaling).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--timesteps T] [--dtype bf16]
+    python bench.py --workload diffwave|wavegrad     # BASELINE configs #3 / #4 (not the headline)
 
 Rank 0 prints one JSON line.  `roofline` is measured with HIP events around every conv3x3
 launch of one extra (untimed) sampling run; `cpu_baseline` times the numpy oracle on a bounded
@@ -52,6 +53,134 @@ def cpu_baseline(B_cpu, k_steps, N, T, threads):
     return B_cpu * N / 16000.0 / (dt * T), dt
 
 
+# spectrogram-conditioned workloads (BASELINE.json configs #3 and #4): config, frames, clips per GPU,
+# step-variant GFLOP per clip and step
+SPEC_WORKLOADS = {
+    "diffwave": dict(config="config_diffwave_bench.json", frames=63, batch=64, bins=513, gflop=31.85,
+                     label="DiffWave config_diffwave.json, linear 1e-4..0.02, T=200, time_step conditioning"),
+    "wavegrad": dict(config="config_wavegrad_bench.json", frames=54, batch=64, bins=128, gflop=47.38,
+                     label="WaveGrad, linear 1e-4..0.05, T=50 (SURVEY §8d fast schedule), sqrt_alpha_bar"),
+}
+
+
+def cpu_baseline_spec(workload, model, spec_np, T, threads):
+    """numpy oracle forward of one clip for one step, extrapolated x T (tests-only restatement)."""
+    sys.path.insert(0, REPO)
+    import numpy as np
+    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    net = model.noise_estimate_model
+    P = {k: v.detach().float().cpu().numpy() for k, v in net.state_dict().items()}
+    spec = spec_np[:1]
+    if workload == "diffwave":
+        from oracle import diffwave as ora
+        x = np.zeros((1, 1, 256 * spec.shape[-1]), np.float32)
+        fn = lambda: ora.forward(P, spec, x, np.array([float(T)], np.float32))   # noqa: E731
+    else:
+        from oracle import wavegrad as ora
+        x = np.zeros((1, 300 * spec.shape[-1]), np.float32)
+        fn = lambda: ora.forward(P, spec, x, np.array([0.5], np.float32))       # noqa: E731
+    t0 = time.perf_counter()
+    fn()
+    dt = time.perf_counter() - t0
+    return x.size / 16000.0 / (dt * T), dt
+
+
+def main_spec(args):
+    """SDDM_spectrogram.infer benches (DiffWave / WaveGrad), same contract as the UNet headline."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from parse_config import ConfigParser, read_json
+    import model.diffusion as module_diffusion
+    import model.network as module_network
+    import model.model as module_arch
+
+    W = SPEC_WORKLOADS[args.workload]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    cfg = read_json(os.path.join(PKG, "configs", W["config"]))
+    if args.timesteps_set:
+        cfg["diffusion"]["args"]["n_timestep"] = args.timesteps
+    config = ConfigParser(cfg)
+    T = cfg["diffusion"]["args"]["n_timestep"]
+    B = args.batch if args.batch_set else W["batch"]
+    F = W["frames"]
+    hop = cfg["spectrogram"]["hop_samples"]
+    N = hop * F
+    torch.manual_seed(0)                                            # random-init weights
+    diffusion = config.init_obj("diffusion", module_diffusion, device=dev)
+    network = config.init_obj("network", module_network, num_samples=N, num_timesteps=T, freq_bins=W["bins"])
+    if args.workload == "diffwave":                                 # SURVEY Q9: output_projection is zero-init
+        with torch.no_grad():
+            network.output_projection.weight.uniform_(-0.1, 0.1)
+    extra = {} if "hop_samples" in cfg["arch"]["args"] else {"hop_samples": hop}    # SURVEY Q6
+    model = config.init_obj("arch", module_arch, diffusion, network, **extra).to(dev).eval()
+    model.compute_dtype = {"bf16": "bfloat16", "f16": "float16", "f32": "float32"}[args.dtype]
+    rng = np.random.default_rng(1234)
+    spec_all = rng.uniform(0, 1, (B * world, W["bins"], F)).astype(np.float32)   # SURVEY §8d: U[0,1]
+    spec = torch.from_numpy(spec_all[rank * B:(rank + 1) * B]).to(dev)
+    gathered = torch.empty((B * world, 1, N), dtype=torch.float32, device=dev)
+
+    def step():
+        out = model.infer(spec, seed=7, row_offset=rank * B)
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, out)
+        else:
+            gathered.copy_(out)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    if not torch.isfinite(gathered).all():
+        raise RuntimeError("non-finite samples")
+    if rank == 0:
+        tfs = args.steps * T * B * W["gflop"] / elapsed / 1e3      # whole-job MFMA rate per GPU
+        cpu = None
+        if not args.no_cpu_baseline:
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+            v, dt = cpu_baseline_spec(args.workload, model, spec_all, T, threads)
+            cpu = {"value": round(v, 6), "unit": "audio_s/s", "cores": threads, "kind": "port",
+                   "sample": f"numpy oracle, 1 network evaluation of 1 clip ({dt:.2f} s), extrapolated x{T}"}
+        audio_s = args.steps * B * world * N / 16000.0
+        line = {"metric": f"denoised audio sec/sec, {T}-step {network.__class__.__name__} @16kHz",
+                "value": round(audio_s / elapsed, 4), "unit": "audio_s/s", "n_gpus": world,
+                "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+                "data": "synthetic spectrograms U[0,1], random-init weights",
+                "config": {"workload": f"{W['label']}, {B}x{N}-sample clips per GPU",
+                           "model": network.__class__.__name__, "global_batch": B * world, "seq_len": N,
+                           "timesteps": T, "parallelism": f"dp{world}"},
+                "roofline": {"bound": "mfma", "achieved": round(tfs, 2),
+                             "peak": MFMA_PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
+                             "frac": round(tfs / MFMA_PEAK_TFLOPS[args.dtype], 4), "traffic": None,
+                             "kernel": "whole sampling run (step-variant algorithmic FLOPs / wall)"},
+                "cpu_baseline": cpu}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -64,7 +193,13 @@ def main():
     ap.add_argument("--cpu-batch", type=int, default=2)
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--workload", default="unet", choices=["unet", "diffwave", "wavegrad"])
+    import sys as _sys
     args = ap.parse_args()
+    args.batch_set = any(a.startswith("--batch") for a in _sys.argv[1:])
+    args.timesteps_set = any(a.startswith("--timesteps") for a in _sys.argv[1:])
+    if args.workload != "unet":
+        return main_spec(args)
 
     import numpy as np
     import torch
