@@ -111,26 +111,35 @@ __global__ __launch_bounds__(256) void wg_conv_kernel(WGConvArgs a) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  for (int tap = 0; tap < a.K; ++tap) {
-    int tp[4];
-    bool ok[4];
+  // flattened K loop over (tap, 32-channel chunk), operands of step s + 1 loaded before the
+  // MFMAs of step s (register double buffer: the loads' latency hides behind 8 MFMAs per wave)
+  const int ncs = Cin / 32, nsteps = a.K * ncs;
+  auto load_step = [&](int st, Frag<T>* af, Frag<T>* bfr) {
+    const int tap = st / ncs, c0 = (st - tap * ncs) * 32;
+#pragma unroll
+    for (int c = 0; c < 2; ++c) af[c] = load_frag<T>((const char*)(wrow[c] + tap * Cin + c0));
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int t = tt0 + p * 16 + l16;
-      tp[p] = t + (tap - half) * a.dil;
-      ok[p] = t < Tc && tp[p] >= 0 && tp[p] < Tc;
+      const int tp = t + (tap - half) * a.dil;
+      const bool ok = t < Tc && tp >= 0 && tp < Tc;
+      bfr[p] = wg_load_b<T, PRE>(a, src_b, film_b, tp, ok, c0 + g * 8);
     }
-    const int kb = tap * Cin;
-    for (int c0 = 0; c0 < Cin; c0 += 32) {
-      Frag<T> af[2], bfr[4];
+  };
+  Frag<T> af[2], bfr[4];
+  load_step(0, af, bfr);
+  for (int st = 0; st < nsteps; ++st) {
+    Frag<T> an[2], bn[4];
+    if (st + 1 < nsteps) load_step(st + 1, an, bn);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) af[c] = load_frag<T>((const char*)(wrow[c] + kb + c0));
+    for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int p = 0; p < 4; ++p) bfr[p] = wg_load_b<T, PRE>(a, src_b, film_b, tp[p], ok[p], c0 + g * 8);
+      for (int p = 0; p < 4; ++p) mfma_frag(acc[c][p], af[c], bfr[p]);
+    if (st + 1 < nsteps) {
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c) af[c] = an[c];
 #pragma unroll
-        for (int p = 0; p < 4; ++p) mfma_frag(acc[c][p], af[c], bfr[p]);
+      for (int p = 0; p < 4; ++p) bfr[p] = bn[p];
     }
   }
 
@@ -238,6 +247,36 @@ hipError_t launch_wg_first(int dtype, const WGFirstArgs& a, hipStream_t s) {
   if (dtype == DT_F32) hipLaunchKernelGGL(wg_first_kernel<float>, grid, dim3(256), 0, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(wg_first_kernel<bf16_t>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(wg_first_kernel<f16_t>, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- FiLM modulation + leaky_relu (one pass, 8 channels per thread) ----------------
+template <typename T>
+__global__ __launch_bounds__(256) void wg_film_kernel(WGFilmArgs a) {
+#pragma clang fp contract(off)
+  const int cv = a.C / 8;
+  const int64_t total = a.BT * cv;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+    const int64_t bt = i / cv;
+    const int c = (int)(i - bt * cv) * 8;
+    float x[8], sh[8], sc[8];
+    load8<T>((const T*)a.x + bt * a.C + c, x);
+    load8<T>((const T*)a.film + bt * 2 * a.C + c, sh);
+    load8<T>((const T*)a.film + bt * 2 * a.C + a.C + c, sc);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = wg_leaky(sh[j] + sc[j] * x[j]);
+    const Frag<T> f = pack8<T>(x);
+    *(Frag<T>*)((T*)a.out + bt * a.C + c) = f;
+  }
+}
+
+hipError_t launch_wg_film(int dtype, const WGFilmArgs& a, hipStream_t s) {
+  if (a.C % 8) return hipErrorInvalidValue;
+  const int64_t total = a.BT * (a.C / 8);
+  const dim3 grid((unsigned)std::max<int64_t>(1, std::min<int64_t>((total + 255) / 256, 32768)));
+  if (dtype == DT_F32) hipLaunchKernelGGL(wg_film_kernel<float>, grid, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(wg_film_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(wg_film_kernel<f16_t>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

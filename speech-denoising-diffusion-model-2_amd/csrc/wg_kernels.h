@@ -30,6 +30,11 @@ hipError_t launch_wg_conv(int dtype, const WGConvArgs& a, hipStream_t s);
 struct WGFirstArgs { const float* audio; const float* w; const float* b; void* out; int B, N; int* t_dev; };
 hipError_t launch_wg_first(int dtype, const WGFirstArgs& a, hipStream_t s);
 
+// FiLM modulation materialised once per element: u[b][t][c] = leaky_relu(0.2)(shift + scale * x)
+// (wavegrad.py:98-99, 104-105, 107-108); film [B][T][2C] (shift | scale), x / u [B][T][C]
+struct WGFilmArgs { const void* x; const void* film; void* out; int64_t BT; int C; };
+hipError_t launch_wg_film(int dtype, const WGFilmArgs& a, hipStream_t s);
+
 // spectrogram [B][C][F] fp32 -> [B][F][C] (T)
 struct WGSpecArgs { const float* spec; void* out; int B, C, F; };
 hipError_t launch_wg_spec(int dtype, const WGSpecArgs& a, hipStream_t s);

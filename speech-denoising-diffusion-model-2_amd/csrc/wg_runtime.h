@@ -156,7 +156,7 @@ static int wg_prepare(sddm_ctx* c, int B, int F) {
     const std::string s = std::to_string(i);
     const int64_t lin = L[5 - i], lout = L[4 - i];
     buf("u" + s + "b1", lin, wg::kUp[i].h);
-    for (const char* n : {"y0", "x", "z", ""}) buf("u" + s + n, lout, wg::kUp[i].h);
+    for (const char* n : {"y0", "x", "z", "", "m"}) buf("u" + s + n, lout, wg::kUp[i].h);   // m: FiLM-modulated input
   }
   d.aoff["eps"] = A.reserve(sizeof(float) * (size_t)B * L[0]);
   d.aoff["encb"] = A.reserve(sizeof(float) * (size_t)B * WGState::kEncN);
@@ -173,10 +173,20 @@ struct WGConvSpec {
   const char* out;
 };
 
-static int wg_conv(sddm_ctx* c, const WGConvSpec& q, int B, const float* enc, int enc_per_b, const int* t_dev,
+static int wg_conv(sddm_ctx* c, WGConvSpec q, int B, const float* enc, int enc_per_b, const int* t_dev,
                    hipStream_t s) {
   WGState& d = *c->wgs;
   const Arena& W = c->warena;
+  std::string mod;
+  if (q.pre == 2) {          // modulate once into the UBlock's scratch, then a plain conv reads it
+    mod = std::string(q.out).substr(0, 2) + "m";
+    WGFilmArgs fa{d.act.base + d.aoff.at(q.src), d.act.base + d.aoff.at(q.film), d.act.base + d.aoff.at(mod),
+                  (int64_t)B * q.Tc, q.Cin};
+    SDDM_HIP_CHECK(launch_wg_film(c->dtype, fa, s));
+    q.src = mod.c_str();
+    q.pre = 0;
+    q.film = nullptr;
+  }
   WGConvArgs a{};
   a.src = d.act.base + d.aoff.at(q.src); a.src_T = (int)q.src_T; a.src_C = q.src_C; a.map = q.map; a.f = q.f;
   a.Tc = (int)q.Tc; a.Cin = q.Cin; a.K = q.K; a.dil = q.dil; a.pre = q.pre;
