@@ -98,6 +98,16 @@ int sddm_transition(sddm_ctx* ctx, int mode, const float* x_t, const float* eps,
                     const float* cond, int t, int64_t B, int64_t N, uint64_t seed,
                     int64_t row_offset, float* out, void* stream);
 
+/* Replaces diffusion.q_stochastic (mode 0, diffusion.py:225-251) and
+ * q_stochastic_conditional (mode 1, diffusion.py:253-279), the forward-process noising of the
+ * training step.  x0 / y / noise / x_t / combined: [B][N] fp32 device pointers; t: [B] int64
+ * device (drawn by the caller, torch.randint(1, T+1) in the reference); r: [B] fp32 device
+ * uniform draws (mode 0; NULL = t_is_integer).  Outputs: x_t; combined noise (mode 1, nullable);
+ * s_out[B] = the sqrt_alpha_bar sample; level_out[B] = t + r (mode 0, nullable). */
+int sddm_q_sample(sddm_ctx* ctx, int mode, const float* x0, const float* y, const float* noise,
+                  const int64_t* t, const float* r, int64_t B, int64_t N, float* x_t,
+                  float* combined, float* s_out, float* level_out, void* stream);
+
 /* Replaces diffusion.get_x_T / get_x_T_conditional / randn_like (model.py:57-68). */
 int sddm_initial_state(sddm_ctx* ctx, int mode, const float* cond, int64_t B, int64_t N,
                        uint64_t seed, int64_t row_offset, float* out, void* stream);

@@ -106,3 +106,34 @@ def infer_spectrogram(network, tab, spec, hop_samples, noise_condition="sqrt_alp
         z = philox.normal(seed, t, x.shape, row_offset) if t > 1 else None
         x = transition("original", tab, x, t, eps, None, z)
     return x
+
+
+def q_stochastic(tab, x0, noise, t, r=None):
+    """GaussianDiffusion.q_stochastic (diffusion.py:225-251) for given draws t [B] (int) and
+    r [B] (uniform; None = t_is_integer).  Returns x_t, s [B], level [B]."""
+    f32 = np.float32
+    sab = tab["sqrt_alpha_bar"].astype(np.float32)
+    if r is None:
+        s = sab[t]
+        level = t.astype(np.int64)
+    else:
+        la, lb = sab[t - 1], sab[t]
+        s = (la + (r.astype(np.float32) * (lb - la)).astype(f32)).astype(f32)
+        level = (t.astype(np.float32) + r.astype(np.float32)).astype(f32)
+    sh = (-1,) + (1,) * (x0.ndim - 1)
+    sv = s.reshape(sh)
+    x_t = ((sv * x0).astype(f32) + (np.sqrt((f32(1.0) - (sv * sv).astype(f32)).astype(f32)) * noise).astype(f32))
+    return x_t.astype(f32), s, level
+
+
+def q_stochastic_conditional(tab, x0, y, noise, t):
+    """GaussianDiffusion.q_stochastic_conditional (diffusion.py:253-279) for given t [B]."""
+    f32 = np.float32
+    sh = (-1,) + (1,) * (x0.ndim - 1)
+    sab = tab["sqrt_alpha_bar"].astype(f32)[t].reshape(sh)
+    g = (tab["sqrt_delta"].astype(f32)[t].reshape(sh) * noise).astype(f32)
+    c = ((tab["m"].astype(f32)[t].reshape(sh) * sab).astype(f32) * (y - x0).astype(f32)).astype(f32)
+    x_t = (((sab * x0).astype(f32) + c).astype(f32) + g).astype(f32)
+    inv = (f32(1.0) / np.sqrt((f32(1.0) - tab["alpha_bar"].astype(f32)[t]).astype(f32))).astype(f32).reshape(sh)
+    comb = (inv * (c + g).astype(f32)).astype(f32)
+    return x_t, comb, sab.reshape(-1)

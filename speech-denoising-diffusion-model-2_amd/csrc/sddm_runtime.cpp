@@ -23,6 +23,7 @@
 #include "../../include/sddm_hip.h"
 #include "json_mini.h"
 #include "kernels.h"
+#include "q_kernels.h"
 #include "sddm_common.h"
 
 namespace sddm {
@@ -1284,6 +1285,34 @@ int sddm_transition(sddm_ctx* c, int mode, const float* x_t, const float* eps, c
   a.mode = mode; a.x_t = x_t; a.eps = eps; a.cond = cond; a.out = out; a.total = B * N; a.N = N; a.t = t;
   a.co = c->coef(); a.seed = seed; a.row_offset = row_offset;
   SDDM_HIP_CHECK(launch_transition(a, (hipStream_t)stream));
+  return SDDM_OK;
+}
+
+int sddm_q_sample(sddm_ctx* c, int mode, const float* x0, const float* y, const float* noise, const int64_t* t,
+                  const float* r, int64_t B, int64_t N, float* x_t, float* combined, float* s_out, float* level_out,
+                  void* stream) {
+  if (!c || !c->configured) FAIL(SDDM_ERR_STATE, "context not configured");
+  if (mode < 0 || mode > 1) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "q_sample mode %d", mode);
+  if (!x0 || !noise || !t || !x_t || (mode == 1 && !y)) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  if (B < 0 || N < 1) FAIL(SDDM_ERR_INVALID_ARG, "shape B=%lld N=%lld", (long long)B, (long long)N);
+  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  if (!c->warena.base) {  // tables only
+    c->warena.reset();
+    c->off_tables = c->warena.reserve(sizeof(float) * 14 * (c->T + 1));
+    c->off_tdev = c->warena.reserve(64 * kMaxLanes);
+    SDDM_HIP_CHECK(c->warena.commit());
+    c->params_dirty = true;
+    c->tables_dirty = true;
+  }
+  if (c->tables_dirty) {
+    const int rr = upload_tables(c);
+    if (rr) return rr;
+  }
+  QArgs a{};
+  a.mode = mode; a.x0 = x0; a.y = y; a.noise = noise; a.t = t; a.r = r;
+  a.sab = c->dtab(3); a.alpha_bar = c->dtab(2); a.m = c->dtab(8); a.sqrt_delta = c->dtab(9);
+  a.x_t = x_t; a.combined = combined; a.s_out = s_out; a.level_out = level_out; a.B = B; a.N = N;
+  SDDM_HIP_CHECK(launch_q_sample(a, (hipStream_t)stream));
   return SDDM_OK;
 }
 

@@ -95,8 +95,46 @@ class GaussianDiffusion(nn.Module):
         """sqrt(alpha_bar[t]) (diffusion.py:322-326)."""
         return self.sqrt_alpha_bar[t]
 
-    def q_stochastic(self, *args, **kwargs):
-        raise NotImplementedError("training-side q_stochastic is outside the sampling hot path (SURVEY.md §8f)")
+    # ---- forward process (training-side q_sample, diffusion.py:225-279) on the HIP device ----
+    def _q(self, mode, x_0, y, noise, t, r):
+        if not x_0.is_cuda:
+            raise RuntimeError("GaussianDiffusion.q_stochastic runs on the HIP device; move tensors to cuda")
+        b = x_0.shape[0]
+        x0 = x_0.contiguous().float()
+        t_dev = t.reshape(-1).to(device=x0.device, dtype=torch.int64).contiguous()
+        if t_dev.numel() != b or int(t_dev.min()) < 1 or int(t_dev.max()) > self.num_timesteps:
+            raise IndexError("q_stochastic: t must hold one step in [1, num_timesteps] per batch row")
+        r_dev = None if r is None else r.reshape(-1).to(device=x0.device, dtype=torch.float32).contiguous()
+        x_t = torch.empty_like(x0)
+        comb = torch.empty_like(x0) if mode == 1 else None
+        s_out = torch.empty(b, dtype=torch.float32, device=x0.device)
+        lvl = torch.empty(b, dtype=torch.float32, device=x0.device) if mode == 0 else None
+        self._context(x0.device).q_sample(mode, x0, None if y is None else y.contiguous().float(),
+                                          noise.contiguous().float(), t_dev, r_dev, x_t, comb, s_out, lvl)
+        return x_t, comb, s_out, lvl, t_dev
 
-    def q_stochastic_conditional(self, *args, **kwargs):
-        raise NotImplementedError("training-side q_stochastic_conditional is outside the sampling hot path")
+    @torch.no_grad()
+    def q_stochastic(self, x_0, noise, t_is_integer=False, t=None, random_step=None):
+        """x_t = s x_0 + sqrt(1 - s^2) noise with s uniform between sqrt_alpha_bar[t-1] and
+        sqrt_alpha_bar[t] (diffusion.py:225-251).  t / random_step are drawn like the reference
+        (torch.randint / torch.rand on x_0's device) unless given."""
+        b = x_0.shape[0]
+        shape = (b,) + (1,) * (x_0.ndim - 1)
+        if t is None:
+            t = torch.randint(1, self.num_timesteps + 1, [b], device=x_0.device)
+        if not t_is_integer and random_step is None:
+            random_step = torch.rand(b, device=x_0.device)
+        x_t, _, s, lvl, t_dev = self._q(0, x_0, None, noise, t, None if t_is_integer else random_step)
+        level = t_dev.view(shape) if t_is_integer else lvl.view(shape)
+        return x_t, s.view(shape), level
+
+    @torch.no_grad()
+    def q_stochastic_conditional(self, x_0, y, noise, t=None):
+        """x_t = sab[t] x_0 + m[t] sab[t] (y - x_0) + sqrt_delta[t] noise and the combined noise
+        (diffusion.py:253-279)."""
+        b = x_0.shape[0]
+        shape = (b,) + (1,) * (x_0.ndim - 1)
+        if t is None:
+            t = torch.randint(1, self.num_timesteps + 1, shape, device=x_0.device)
+        x_t, comb, s, _, _ = self._q(1, x_0, y, noise, t, None)
+        return x_t, comb, s.view(shape)

@@ -82,6 +82,9 @@ def main():
     from model.UNetModified2 import UNetModified2, PositionalEncoding
     from model.model import SDDM
     out = {}
+    if args.only == "q":
+        gen_q(torch, GaussianDiffusion, args.out)
+        return
     if args.only == "wavegrad":
         gen_wavegrad(torch, philox, make_params, GaussianDiffusion, args.out)
         return
@@ -244,7 +247,33 @@ def main():
     np.savez_compressed(os.path.join(args.out, "diffwave.npz"), **dw)
     np.savez_compressed(os.path.join(args.out, "embedding.npz"), **emb)
     gen_wavegrad(torch, philox, make_params, GaussianDiffusion, args.out)
+    gen_q(torch, GaussianDiffusion, args.out)
     print("wrote fixtures to", args.out)
+
+
+def gen_q(torch, GaussianDiffusion, out_dir):
+    """9. Forward-process noising q_stochastic / q_stochastic_conditional (diffusion.py:225-279):
+    torch.manual_seed(s) before each call fixes the reference's randint / rand draws (CPU
+    generator), which the tests re-draw with the same seed and hand to the library."""
+    q = {}
+    rng = np.random.default_rng(21)
+    for sched in (("linear", 50, 1e-6, 1e-3), ("linear", 200, 1e-4, 0.02)):
+        d = GaussianDiffusion(*sched, device="cpu")
+        B, N = 4, 700
+        x0 = rng.uniform(-0.5, 0.5, (B, 1, N)).astype(np.float32)
+        y = (x0 + rng.uniform(-0.2, 0.2, (B, 1, N))).astype(np.float32)
+        noise = rng.standard_normal((B, 1, N)).astype(np.float32)
+        k = f"q/{sched_key(sched)}"
+        q[k + "/x0"], q[k + "/y"], q[k + "/noise"] = x0, y, noise
+        with torch.no_grad():
+            for ti, name in ((False, "float"), (True, "int")):
+                torch.manual_seed(5)
+                xt, s, lvl = d.q_stochastic(torch.from_numpy(x0), torch.from_numpy(noise), t_is_integer=ti)
+                q[f"{k}/{name}/x_t"], q[f"{k}/{name}/s"], q[f"{k}/{name}/level"] = xt.numpy(), s.numpy(), lvl.numpy()
+            torch.manual_seed(6)
+            xt, comb, s = d.q_stochastic_conditional(torch.from_numpy(x0), torch.from_numpy(y), torch.from_numpy(noise))
+            q[f"{k}/cond/x_t"], q[f"{k}/cond/combined"], q[f"{k}/cond/s"] = xt.numpy(), comb.numpy(), s.numpy()
+    np.savez_compressed(os.path.join(out_dir, "q_sample.npz"), **q)
 
 
 def gen_wavegrad(torch, philox, make_params, GaussianDiffusion, out_dir):

@@ -176,3 +176,33 @@ def test_wavegrad_oracle_sampling_matches_reference():
     out = sampler.infer_spectrogram(lambda s, x, nl: wg.forward(P, s, x[:, 0], nl)[:, None], tab, z[f"{k}/spec"],
                                     wg.HOP, noise_condition="sqrt_alpha_bar", seed=7)
     assert rms(out, z[f"{k}/out"]) <= 1e-5
+
+
+# ---------------- forward process q_stochastic (diffusion.py:225-279) ----------------
+def _q_draws(T, B, seed, integer=False, cond=False):
+    import torch
+    torch.manual_seed(seed)
+    if cond:
+        return torch.randint(1, T + 1, (B, 1, 1)).reshape(-1).numpy(), None
+    t = torch.randint(1, T + 1, [B]).numpy()
+    return t, (None if integer else torch.rand(B).numpy())
+
+
+@pytest.mark.parametrize("sk", ["linear_50_1e-06_0.001", "linear_200_0.0001_0.02"])
+def test_q_stochastic_oracle_matches_reference(sk):
+    z = golden("q_sample.npz")
+    tab = tables_from_golden(sk)
+    T = parse_sched_key(sk)[1]
+    k = f"q/{sk}"
+    x0, y, noise = z[k + "/x0"], z[k + "/y"], z[k + "/noise"]
+    for name, integer in (("float", False), ("int", True)):
+        t, r = _q_draws(T, x0.shape[0], 5, integer)
+        x_t, s, lvl = sampler.q_stochastic(tab, x0, noise, t, r)
+        assert np.abs(x_t - z[f"{k}/{name}/x_t"]).max() <= 1e-6
+        assert np.array_equal(s, z[f"{k}/{name}/s"].reshape(-1))
+        assert np.array_equal(lvl, z[f"{k}/{name}/level"].reshape(-1))
+    t, _ = _q_draws(T, x0.shape[0], 6, cond=True)
+    x_t, comb, s = sampler.q_stochastic_conditional(tab, x0, y, noise, t)
+    ok = np.isfinite(z[f"{k}/cond/x_t"])
+    assert np.abs(x_t - z[f"{k}/cond/x_t"])[ok].max() <= 1e-6
+    assert np.abs(comb - z[f"{k}/cond/combined"])[ok].max() <= 1e-5
