@@ -15,6 +15,8 @@
 #include "conv_common.h"
 #include "wg_kernels.h"
 
+#include <cstdlib>
+
 namespace sddm {
 
 constexpr int WG_MC = 64;    // output channels per block
@@ -183,8 +185,152 @@ __global__ __launch_bounds__(256) void wg_conv_kernel(WGConvArgs a) {
   }
 }
 
+// ---------------- LDS-staged variant for Cout % 128 == 0 ----------------
+// Block = 4 waves = 128 output channels x 128 positions; wave w owns channels [64 (w & 1), +64) x
+// positions [64 (w >> 1), +64) as 4 x 4 MFMA tiles.  Per 32-channel chunk of the input the block
+// stages (a) the transformed input slab of 128 + 2 * halo rows once (index map, zero padding and
+// leaky applied here, once per element) and (b) the weights of all KT taps for its 128 channels;
+// every tap then reads its B fragments from the slab at a row offset of tap * dil.  The next
+// chunk's global loads are issued before the current chunk's MFMAs.
+constexpr int WGL_MC = 128, WGL_MT = 128, WGL_HALO = 8;
+
+template <typename T, int PRE, int KT>
+__global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
+#pragma clang fp contract(off)
+  constexpr int ES = (int)sizeof(T), UE = 16 / ES;         // elements per 16-byte unit
+  constexpr int UPR = 32 / UE;                              // units per 32-channel row
+  constexpr int RS = UPR * 16 + 16;                         // padded LDS row stride (bytes)
+  constexpr int SROWS = WGL_MT + 2 * WGL_HALO;
+  constexpr int NBU = SROWS * UPR, NAU = KT * WGL_MC * UPR;
+  constexpr int PB = (NBU + 255) / 256, PA = (NAU + 255) / 256;
+  __shared__ __attribute__((aligned(16))) char lds[(SROWS + KT * WGL_MC) * RS];
+  char* slab = lds;
+  char* wl = lds + SROWS * RS;
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int b = blockIdx.z, cob = blockIdx.y * WGL_MC, t0 = blockIdx.x * WGL_MT;
+  const int Tc = a.Tc, Cin = a.Cin, half = (KT - 1) / 2, H = half * a.dil;
+  const int rows = WGL_MT + 2 * H;
+  const T* src_b = (const T*)a.src + (size_t)b * a.src_T * a.src_C;
+  const T* W = (const T*)a.w;
+
+  f32x4 breg[PB], areg[PA];
+  auto gload = [&](int c0) {
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int u = tid + j * 256;
+      const int r = u / UPR, q = u - r * UPR;
+      const int tp = t0 - H + r;
+      breg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (u < rows * UPR && tp >= 0 && tp < Tc)
+        breg[j] = *(const f32x4*)(src_b + (size_t)wg_map(tp, a.map, a.f) * a.src_C + c0 + q * UE);
+    }
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int u = tid + j * 256;
+      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
+      if (u < NAU) areg[j] = *(const f32x4*)(W + ((size_t)(cob + co) * KT + k) * Cin + c0 + q * UE);
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int j = 0; j < PB; ++j) {
+      const int u = tid + j * 256;
+      if (u >= rows * UPR) continue;
+      const int r = u / UPR, q = u - r * UPR;
+      f32x4 v = breg[j];
+      if (PRE == 1) {
+        typedef T vec __attribute__((ext_vector_type(UE)));
+        vec x = __builtin_bit_cast(vec, v);
+#pragma unroll
+        for (int e = 0; e < UE; ++e) x[e] = from_f32<T>(wg_leaky(to_f32<T>(x[e])));
+        v = __builtin_bit_cast(f32x4, x);
+      }
+      *(f32x4*)(slab + r * RS + q * 16) = v;
+    }
+#pragma unroll
+    for (int j = 0; j < PA; ++j) {
+      const int u = tid + j * 256;
+      if (u >= NAU) continue;
+      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
+      *(f32x4*)(wl + (k * WGL_MC + co) * RS + q * 16) = areg[j];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[i][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int wc = (wave & 1) * 64, wt = (wave >> 1) * 64;
+  const int ncs = Cin / 32;
+  gload(0);
+  for (int cc = 0; cc < ncs; ++cc) {
+    __syncthreads();
+    lstore();
+    __syncthreads();
+    if (cc + 1 < ncs) gload((cc + 1) * 32);
+#pragma unroll
+    for (int k = 0; k < KT; ++k) {
+      Frag<T> af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = load_frag<T>(wl + (k * WGL_MC + wc + i * 16 + l16) * RS + g * 8 * ES);
+#pragma unroll
+      for (int p = 0; p < 4; ++p) bf[p] = load_frag<T>(slab + (wt + p * 16 + l16 + k * a.dil) * RS + g * 8 * ES);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int p = 0; p < 4; ++p) mfma_frag(acc[i][p], af[i], bf[p]);
+    }
+  }
+
+  const float* enc = nullptr;
+  if (a.post == 1) {
+    const int row = a.enc_per_b ? b : *a.t_dev;
+    enc = a.enc + (size_t)row * a.enc_stride + a.enc_off;
+  }
+  const T* res_b = a.res ? (const T*)a.res + (size_t)b * a.res_T * a.Cout : nullptr;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int cb = cob + wc + i * 16 + 4 * g;
+    float bias[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[e] = a.bias[cb + e];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int t = t0 + wt + p * 16 + l16;
+      if (t >= Tc) continue;
+      float v[4];
+      f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (res_b) rv = load4<T>(res_b + (size_t)wg_map(t, a.res_map, a.res_f) * a.Cout + cb);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float x = acc[i][p][e] + bias[e];
+        if (a.post == 1) x = wg_leaky(x) + enc[cb + e];
+        if (res_b) x = x + rv[e];
+        v[e] = x;
+      }
+      store4<T>((T*)a.out + ((size_t)b * Tc + t) * a.Cout + cb, v[0], v[1], v[2], v[3]);
+    }
+  }
+}
+
+template <typename T, int PRE>
+static void wg_conv_lds_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
+  if (a.K == 1) hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 1>), grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3>), grid, dim3(256), 0, s, a);
+}
+
 template <typename T>
 static void wg_conv_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
+  if (a.Cout % WGL_MC == 0 && !a.out_f32 && a.pre != 2 && (a.K == 1 || (a.K == 3 && a.dil <= WGL_HALO)) &&
+      !std::getenv("SDDM_WG_NO_LDS")) {
+    const dim3 g2((a.Tc + WGL_MT - 1) / WGL_MT, a.Cout / WGL_MC, a.B);
+    if (a.pre == 0) wg_conv_lds_dispatch<T, 0>(a, g2, s);
+    else wg_conv_lds_dispatch<T, 1>(a, g2, s);
+    return;
+  }
   if (a.pre == 0) hipLaunchKernelGGL((wg_conv_kernel<T, 0>), grid, dim3(256), 0, s, a);
   else if (a.pre == 1) hipLaunchKernelGGL((wg_conv_kernel<T, 1>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((wg_conv_kernel<T, 2>), grid, dim3(256), 0, s, a);
