@@ -215,7 +215,9 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
   const T* src_b = (const T*)a.src + (size_t)b * a.src_T * a.src_C;
   const T* W = (const T*)a.w;
 
-  f32x4 breg[PB], areg[PA];
+  constexpr int PF = PRE == 2 ? PB : 1;
+  f32x4 breg[PB], areg[PA], shreg[PF], screg[PF];
+  const T* film_b = PRE == 2 ? (const T*)a.film + (size_t)b * Tc * 2 * Cin : nullptr;
   auto gload = [&](int c0) {
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
@@ -223,8 +225,13 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
       const int r = u / UPR, q = u - r * UPR;
       const int tp = t0 - H + r;
       breg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (u < rows * UPR && tp >= 0 && tp < Tc)
-        breg[j] = *(const f32x4*)(src_b + (size_t)wg_map(tp, a.map, a.f) * a.src_C + c0 + q * UE);
+      const bool in = u < rows * UPR && tp >= 0 && tp < Tc;
+      if (in) breg[j] = *(const f32x4*)(src_b + (size_t)wg_map(tp, a.map, a.f) * a.src_C + c0 + q * UE);
+      if (PRE == 2 && in) {               // FiLM shift / scale at the conv-input position
+        const T* fp = film_b + (size_t)tp * 2 * Cin + c0 + q * UE;
+        shreg[j % PF] = *(const f32x4*)fp;
+        screg[j % PF] = *(const f32x4*)(fp + Cin);
+      }
     }
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
@@ -240,11 +247,19 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
       if (u >= rows * UPR) continue;
       const int r = u / UPR, q = u - r * UPR;
       f32x4 v = breg[j];
+      const int tp = t0 - H + r;
       if (PRE == 1) {
         typedef T vec __attribute__((ext_vector_type(UE)));
         vec x = __builtin_bit_cast(vec, v);
 #pragma unroll
         for (int e = 0; e < UE; ++e) x[e] = from_f32<T>(wg_leaky(to_f32<T>(x[e])));
+        v = __builtin_bit_cast(f32x4, x);
+      } else if (PRE == 2 && tp >= 0 && tp < Tc) {   // leaky(shift + scale * x); padding stays 0
+        typedef T vec __attribute__((ext_vector_type(UE)));
+        vec x = __builtin_bit_cast(vec, v);
+        const vec sh = __builtin_bit_cast(vec, shreg[j % PF]), sc = __builtin_bit_cast(vec, screg[j % PF]);
+#pragma unroll
+        for (int e = 0; e < UE; ++e) x[e] = from_f32<T>(wg_leaky(to_f32<T>(sh[e]) + to_f32<T>(sc[e]) * to_f32<T>(x[e])));
         v = __builtin_bit_cast(f32x4, x);
       }
       *(f32x4*)(slab + r * RS + q * 16) = v;
@@ -316,19 +331,25 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
   }
 }
 
+bool wg_conv_uses_lds(const WGConvArgs& a) {
+  static const bool off = std::getenv("SDDM_WG_NO_LDS") != nullptr;
+  return !off && a.Cout % WGL_MC == 0 && !a.out_f32 && (a.K == 3 && a.dil <= WGL_HALO) ||
+         (!off && a.Cout % WGL_MC == 0 && !a.out_f32 && a.K == 1 && a.pre != 2);
+}
+
 template <typename T, int PRE>
 static void wg_conv_lds_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
-  if (a.K == 1) hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 1>), grid, dim3(256), 0, s, a);
+  if (a.K == 1) hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE == 2 ? 0 : PRE, 1>), grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3>), grid, dim3(256), 0, s, a);
 }
 
 template <typename T>
 static void wg_conv_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
-  if (a.Cout % WGL_MC == 0 && !a.out_f32 && a.pre != 2 && (a.K == 1 || (a.K == 3 && a.dil <= WGL_HALO)) &&
-      !std::getenv("SDDM_WG_NO_LDS")) {
+  if (wg_conv_uses_lds(a)) {
     const dim3 g2((a.Tc + WGL_MT - 1) / WGL_MT, a.Cout / WGL_MC, a.B);
     if (a.pre == 0) wg_conv_lds_dispatch<T, 0>(a, g2, s);
-    else wg_conv_lds_dispatch<T, 1>(a, g2, s);
+    else if (a.pre == 1) wg_conv_lds_dispatch<T, 1>(a, g2, s);
+    else wg_conv_lds_dispatch<T, 2>(a, g2, s);
     return;
   }
   if (a.pre == 0) hipLaunchKernelGGL((wg_conv_kernel<T, 0>), grid, dim3(256), 0, s, a);

@@ -24,6 +24,8 @@ struct WGConvArgs {
   int B;
 };
 hipError_t launch_wg_conv(int dtype, const WGConvArgs& a, hipStream_t s);
+// true when launch_wg_conv takes the LDS-staged kernel (which applies pre == 2 itself)
+bool wg_conv_uses_lds(const WGConvArgs& a);
 
 // downsample.0: Conv1d(1, 32, 5, padding=2) on the fp32 audio [B][N] -> [B][N][32] (T); decrements
 // the device step counter (one launch per reverse step)

@@ -178,7 +178,9 @@ static int wg_conv(sddm_ctx* c, WGConvSpec q, int B, const float* enc, int enc_p
   WGState& d = *c->wgs;
   const Arena& W = c->warena;
   std::string mod;
-  if (q.pre == 2) {          // modulate once into the UBlock's scratch, then a plain conv reads it
+  WGConvArgs probe{};
+  probe.Cout = q.Cout; probe.K = q.K; probe.dil = q.dil; probe.pre = q.pre; probe.out_f32 = 0;
+  if (q.pre == 2 && !wg_conv_uses_lds(probe)) {   // modulate once into the UBlock's scratch, then a plain conv
     mod = std::string(q.out).substr(0, 2) + "m";
     WGFilmArgs fa{d.act.base + d.aoff.at(q.src), d.act.base + d.aoff.at(q.film), d.act.base + d.aoff.at(mod),
                   (int64_t)B * q.Tc, q.Cin};
