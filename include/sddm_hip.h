@@ -108,6 +108,14 @@ int sddm_q_sample(sddm_ctx* ctx, int mode, const float* x0, const float* y, cons
                   const int64_t* t, const float* r, int64_t B, int64_t N, float* x_t,
                   float* combined, float* s_out, float* level_out, void* stream);
 
+/* Replaces the torchaudio featurizer of prepare_spectrogram.py:20-55 (context-free):
+ * out[B][n_out][1 + N/hop] = clamp((log10(S) - 1 + 5) / 5, 0, 1), S = |STFT| (center, reflect
+ * padding, `window` [n_fft], power 1, normalized by sqrt(sum window^2)); with fb
+ * ([n_fft/2+1][n_out], nullable) S is projected onto the mel filterbank first.  All pointers are
+ * device pointers; n_fft a power of two <= 1024. */
+int sddm_log_spectrogram(const float* audio, int64_t B, int64_t N, int n_fft, int hop,
+                         const float* window, const float* fb, int n_out, float* out, void* stream);
+
 /* Replaces diffusion.get_x_T / get_x_T_conditional / randn_like (model.py:57-68). */
 int sddm_initial_state(sddm_ctx* ctx, int mode, const float* cond, int64_t B, int64_t N,
                        uint64_t seed, int64_t row_offset, float* out, void* stream);

@@ -24,6 +24,7 @@
 #include "json_mini.h"
 #include "kernels.h"
 #include "q_kernels.h"
+#include "stft_kernels.h"
 #include "sddm_common.h"
 
 namespace sddm {
@@ -1313,6 +1314,19 @@ int sddm_q_sample(sddm_ctx* c, int mode, const float* x0, const float* y, const 
   a.sab = c->dtab(3); a.alpha_bar = c->dtab(2); a.m = c->dtab(8); a.sqrt_delta = c->dtab(9);
   a.x_t = x_t; a.combined = combined; a.s_out = s_out; a.level_out = level_out; a.B = B; a.N = N;
   SDDM_HIP_CHECK(launch_q_sample(a, (hipStream_t)stream));
+  return SDDM_OK;
+}
+
+int sddm_log_spectrogram(const float* audio, int64_t B, int64_t N, int n_fft, int hop, const float* window,
+                         const float* fb, int n_out, float* out, void* stream) {
+  if (!audio || !window || !out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
+  if (n_fft < 2 || n_fft > 1024 || (n_fft & (n_fft - 1))) FAIL(SDDM_ERR_NOT_IMPLEMENTED, "n_fft %d (powers of two <= 1024)", n_fft);
+  if (hop < 1 || B < 1 || N <= n_fft / 2) FAIL(SDDM_ERR_SHAPE, "B=%lld N=%lld hop=%d n_fft=%d", (long long)B, (long long)N, hop, n_fft);
+  if (!fb && n_out != n_fft / 2 + 1) FAIL(SDDM_ERR_INVALID_ARG, "linear spectrogram has %d bins, not %d", n_fft / 2 + 1, n_out);
+  StftArgs a{};
+  a.audio = audio; a.B = B; a.N = N; a.n_fft = n_fft; a.hop = hop; a.frames = (int)(1 + N / hop); a.n_out = n_out;
+  a.window = window; a.fb = fb; a.out = out;
+  SDDM_HIP_CHECK(launch_stft_features(a, (hipStream_t)stream));
   return SDDM_OK;
 }
 

@@ -25,7 +25,7 @@ TABLE_NAMES = ("betas", "alphas", "alpha_bar", "sqrt_alpha_bar", "predicted_nois
 EXPORTS = ("sddm_abi_version", "sddm_last_error", "sddm_create", "sddm_destroy", "sddm_configure",
            "sddm_load_param", "sddm_missing_params", "sddm_sample", "sddm_sample_continuous",
            "sddm_network_forward",
-           "sddm_transition", "sddm_q_sample", "sddm_initial_state", "sddm_schedule", "sddm_profile_enable",
+           "sddm_transition", "sddm_q_sample", "sddm_log_spectrogram", "sddm_initial_state", "sddm_schedule", "sddm_profile_enable",
            "sddm_profile_read", "sddm_profile_ops")
 
 _lib = None
@@ -53,6 +53,7 @@ def lib():
         L.sddm_network_forward.argtypes = [vp, vp, vp, vp, i64, i64, vp, vp]
         L.sddm_transition.argtypes = [vp, c_int, vp, vp, vp, c_int, i64, i64, u64, i64, vp, vp]
         L.sddm_q_sample.argtypes = [vp, c_int, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp]
+        L.sddm_log_spectrogram.argtypes = [vp, i64, i64, c_int, c_int, vp, vp, c_int, vp, vp]
         L.sddm_initial_state.argtypes = [vp, c_int, vp, i64, i64, u64, i64, vp, vp]
         L.sddm_schedule.argtypes = [ctypes.c_char_p, c_int, ctypes.c_double, ctypes.c_double, vp]
         L.sddm_profile_enable.argtypes = [vp, c_int]
@@ -193,3 +194,12 @@ class Context:
         buf = ctypes.create_string_buffer(1 << 20)
         check(lib().sddm_profile_ops(self._h, buf, len(buf)))
         return json.loads(buf.value.decode())
+
+
+def log_spectrogram(audio, n_fft, hop, window, fb, n_out, out):
+    """sddm_log_spectrogram on CUDA tensors (audio [B, N], window [n_fft], fb [n_fft/2+1, n_out] or
+    None, out [B, n_out, 1 + N // hop])."""
+    import torch
+    B, N = audio.shape
+    check(lib().sddm_log_spectrogram(_ptr(audio), B, N, int(n_fft), int(hop), _ptr(window), _ptr(fb), int(n_out),
+                                     _ptr(out), _stream(torch, audio.device)))

@@ -82,6 +82,9 @@ def main():
     from model.UNetModified2 import UNetModified2, PositionalEncoding
     from model.model import SDDM
     out = {}
+    if args.only == "stft":
+        gen_stft(torch, args.out)
+        return
     if args.only == "q":
         gen_q(torch, GaussianDiffusion, args.out)
         return
@@ -248,7 +251,32 @@ def main():
     np.savez_compressed(os.path.join(args.out, "embedding.npz"), **emb)
     gen_wavegrad(torch, philox, make_params, GaussianDiffusion, args.out)
     gen_q(torch, GaussianDiffusion, args.out)
+    gen_stft(torch, args.out)
     print("wrote fixtures to", args.out)
+
+
+def gen_stft(torch, out_dir):
+    """10. prepare_spectrogram.py:20-55 features.  torchaudio is absent, so the fixture restates
+    torchaudio.functional.spectrogram with torch.stft (center, reflect, onesided, 'window'
+    normalisation, power 1) and MelScale with the facade's melscale_fbanks (torch fp32 ops)."""
+    from features import melscale_fbanks
+    from sddm_hip.synth import noisy_speech
+    st = {}
+    audio = noisy_speech(2, 4000, seed=3).reshape(2, -1).astype(np.float32)
+    audio[1, 1000:1400] = 0.0                                      # exact-zero stretch (log10(0) edge)
+    x = torch.from_numpy(audio)
+    w = torch.hamming_window(1024)
+    spec = torch.stft(x, 1024, 256, 1024, w, center=True, pad_mode="reflect", normalized=False, onesided=True,
+                      return_complex=True)
+    spec = spec / w.pow(2.).sum().sqrt()
+    mag = spec.abs()
+    fb = melscale_fbanks(513, 20.0, 8000.0, 128, 16000)
+    mel = torch.matmul(mag.transpose(-1, -2), fb).transpose(-1, -2)
+    for name, S in (("spec", mag), ("mel", mel)):
+        v = torch.log10(S) - 1
+        st[f"stft/{name}"] = torch.clamp((v + 5) / 5, 0.0, 1.0).numpy()
+    st["stft/audio"], st["stft/fb"], st["stft/window"] = audio, fb.numpy(), w.numpy()
+    np.savez_compressed(os.path.join(out_dir, "stft.npz"), **st)
 
 
 def gen_q(torch, GaussianDiffusion, out_dir):

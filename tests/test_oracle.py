@@ -206,3 +206,14 @@ def test_q_stochastic_oracle_matches_reference(sk):
     ok = np.isfinite(z[f"{k}/cond/x_t"])
     assert np.abs(x_t - z[f"{k}/cond/x_t"])[ok].max() <= 1e-6
     assert np.abs(comb - z[f"{k}/cond/combined"])[ok].max() <= 1e-5
+
+
+# ---------------- spectrogram featurizer (prepare_spectrogram.py:20-55) ----------------
+def test_featurizer_oracle_matches_stft_fixture():
+    from oracle import features as fe
+    z = golden("stft.npz")
+    assert np.abs(fe.hamming(1024) - z["stft/window"]).max() <= 1e-6
+    for name, fb in (("spec", None), ("mel", z["stft/fb"])):
+        out = fe.log_spectrogram(z["stft/audio"], fb=fb, window=z["stft/window"])
+        assert out.shape == z[f"stft/{name}"].shape
+        assert np.abs(out - z[f"stft/{name}"]).max() <= 1e-5
