@@ -204,17 +204,17 @@ hipError_t launch_dw_input(int dtype, const DWInArgs& a, hipStream_t s) {
 
 // ---------------- fused residual layer ----------------
 template <typename T>
-__global__ __launch_bounds__(256) void dw_layer_kernel(DWLayerArgs a) {
+__global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
   constexpr int ES = (int)sizeof(T), VE = 16 / ES;
   constexpr int UPS = DW_C / VE;                  // 16-byte units (planes) per sample and tap
   constexpr int PB = 64 / UPS;                    // samples per 64-unit staging group
   constexpr int PLANE = DW_MS * 16;               // bytes per plane (2 KB, = 0 mod 256)
   constexpr int NU = 3 * DW_MS * UPS;             // staged units
-  constexpr int MAXU = 12;
+  constexpr int MAXU = 4;
   typedef T vec4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* yin = smem;                               // [3 taps][UPS][128 samples][16 B]
-  char* zl = smem + 3 * UPS * PLANE;              // [UPS][128 samples][16 B]
+  char* zl = smem;                                // [UPS][128 samples][16 B], aliases yin after GEMM 1
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -223,19 +223,7 @@ __global__ __launch_bounds__(256) void dw_layer_kernel(DWLayerArgs a) {
   const int row = a.ds_per_b ? b : (a.t_dev ? *a.t_dev : 0);
   const float* ds = a.ds + ((size_t)row * a.L + a.layer) * DW_C;
 
-  // conditioner + bias of this lane's gate / filter rows (issued first, used after the GEMM)
   const int cg = wave * 16 + 4 * g;               // gate row base; filter rows cg + 64
-  vec4 cnd[2][8];
-  {
-    const T* cb = (const T*)a.cond + a.layer * 128;
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int n = min(n0 + p * 16 + (lane & 15), N - 1);
-      const T* cp = cb + ((size_t)b * N + n) * a.L * 128;
-      cnd[0][p] = *(const vec4*)(cp + cg);
-      cnd[1][p] = *(const vec4*)(cp + cg + 64);
-    }
-  }
   // ---- 1. y = x + diffusion projection at the three taps -> LDS ----
   for (int u0 = 0; u0 < NU; u0 += MAXU * 256) {
     f32x4 reg[MAXU];
@@ -263,6 +251,18 @@ __global__ __launch_bounds__(256) void dw_layer_kernel(DWLayerArgs a) {
     }
   }
   __syncthreads();
+  // conditioner + bias of this lane's gate / filter rows (issued before GEMM 1, used after it)
+  vec4 cnd[2][8];
+  {
+    const T* cb = (const T*)a.cond + a.layer * 128;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int n = min(n0 + p * 16 + (lane & 15), N - 1);
+      const T* cp = cb + ((size_t)b * N + n) * a.L * 128;
+      cnd[0][p] = *(const vec4*)(cp + cg);
+      cnd[1][p] = *(const vec4*)(cp + cg + 64);
+    }
+  }
   // ---- 2. dilated conv GEMM: rows {16w.., 64+16w..} x 128 samples, K = 192 ----
   f32x4 acc[2][8];
 #pragma unroll
@@ -285,7 +285,8 @@ __global__ __launch_bounds__(256) void dw_layer_kernel(DWLayerArgs a) {
       for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], af[c], bf);
     }
   }
-  // ---- gated activation z = sigmoid(gate) * tanh(filter) -> LDS (plane-major) ----
+  // ---- gated activation z = sigmoid(gate) * tanh(filter) -> LDS (plane-major, over yin) ----
+  __syncthreads();                                // every wave is done reading yin
   {
     float bg[4], bfl[4];
 #pragma unroll
@@ -350,7 +351,7 @@ __global__ __launch_bounds__(256) void dw_layer_kernel(DWLayerArgs a) {
 
 size_t dw_layer_lds_bytes(int dtype) {
   const int ups = DW_C * (dtype == DT_F32 ? 4 : 2) / 16;
-  return (size_t)4 * ups * DW_MS * 16;
+  return (size_t)3 * ups * DW_MS * 16;
 }
 
 hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
