@@ -302,37 +302,29 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
       }
       char* zp = zl + (cg / VE) * PLANE + (p * 16 + (lane & 15)) * 16 + (cg % VE) * ES;
       store4<T>((T*)zp, z[0], z[1], z[2], z[3]);
+      const int n = n0 + p * 16 + (lane & 15);      // z of every layer, for the deferred skip GEMM
+      if (n < N) store4<T>((T*)a.z + (((size_t)b * N + n) * a.L + a.layer) * DW_C + cg, z[0], z[1], z[2], z[3]);
     }
   }
   __syncthreads();
-  // ---- 3. output_residual / output_projection GEMM: rows {16w.. residual, 64+16w.. skip}, K = 64 ----
+  // ---- 3. output_residual GEMM: rows 16w.., K = 64 (output_projection is deferred: dw_skip_kernel) ----
 #pragma unroll
-  for (int c = 0; c < 2; ++c)
-#pragma unroll
-    for (int p = 0; p < 8; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < 8; ++p) acc[0][p] = f32x4{0.f, 0.f, 0.f, 0.f};
   const T* w2 = (const T*)a.w2;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    Frag<T> af[2];
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      af[c] = load_frag<T>((const char*)(w2 + (size_t)(c * 64 + wave * 16 + (lane & 15)) * DW_C + s * 32 + g * 8));
+    const Frag<T> af = load_frag<T>((const char*)(w2 + (size_t)(wave * 16 + (lane & 15)) * DW_C + s * 32 + g * 8));
     const char* pb = zl + ((s * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const Frag<T> bf = load_planes<T>(pb + p * 256, PLANE);
-#pragma unroll
-      for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], af[c], bf);
-    }
+    for (int p = 0; p < 8; ++p) mfma_frag(acc[0][p], af, load_planes<T>(pb + p * 256, PLANE));
   }
-  // ---- epilogue: x_out = (x + residual) / sqrt(2), skip (+)= skip ----
+  // ---- epilogue: x_out = (x + residual) / sqrt(2) ----
   {
     const float r2 = 1.41421353816986083984375f;   // (float)sqrt(2.0) (diffwave.py:108)
-    float br[4], bs[4];
+    float br[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { br[i] = a.b2[cg + i]; bs[i] = a.b2[64 + cg + i]; }
+    for (int i = 0; i < 4; ++i) br[i] = a.b2[cg + i];
     T* xo = (T*)a.x_out + (size_t)b * N * DW_C;
-    float* sk = a.skip + (size_t)b * N * DW_C;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       const int n = n0 + p * 16 + (lane & 15);
@@ -341,10 +333,6 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
       store4<T>(xo + (size_t)n * DW_C + cg, (to_f32<T>(xv[0]) + (acc[0][p][0] + br[0])) / r2,
                 (to_f32<T>(xv[1]) + (acc[0][p][1] + br[1])) / r2, (to_f32<T>(xv[2]) + (acc[0][p][2] + br[2])) / r2,
                 (to_f32<T>(xv[3]) + (acc[0][p][3] + br[3])) / r2);
-      f32x4* sp = (f32x4*)(sk + (size_t)n * DW_C + cg);
-      f32x4 v = f32x4{acc[1][p][0] + bs[0], acc[1][p][1] + bs[1], acc[1][p][2] + bs[2], acc[1][p][3] + bs[3]};
-      if (!a.first) v = *sp + v;
-      *sp = v;
     }
   }
 }
@@ -360,6 +348,57 @@ hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
   if (dtype == DT_F32) hipLaunchKernelGGL(dw_layer_kernel<float>, grid, dim3(256), lds, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_layer_kernel<bf16_t>, grid, dim3(256), lds, s, a);
   else hipLaunchKernelGGL(dw_layer_kernel<f16_t>, grid, dim3(256), lds, s, a);
+  return hipGetLastError();
+}
+
+// ---------------- deferred skip sum: skip[b][n][co] = sum_l Wo_l z_l + sum_l bo_l (K = L x 64) ----------------
+// diffwave.py:104-106, 150-152: every layer's output_projection applied to its stored gated
+// activation z_l [B][N][L][64] in one GEMM instead of a per-layer fp32 read-modify-write.
+template <typename T>
+__global__ __launch_bounds__(256) void dw_skip_kernel(DWSkipArgs a) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int n0 = blockIdx.x * DW_MS, b = blockIdx.y, K = a.L * DW_C;
+  const T* arow = (const T*)a.w + (size_t)(wave * 16 + (lane & 15)) * K + g * 8;
+  const T* Z = (const T*)a.z + (size_t)b * a.N * K;
+  const T* brow[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) brow[p] = Z + (size_t)min(n0 + p * 16 + (lane & 15), a.N - 1) * K + g * 8;
+  f32x4 acc[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag<T> af = load_frag<T>((const char*)arow), bf[8];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) bf[p] = load_frag<T>((const char*)brow[p]);
+  for (int k = 0; k < K; k += 32) {
+    Frag<T> an, bn[8];
+    const int kn = k + 32 < K ? k + 32 : k;
+    an = load_frag<T>((const char*)(arow + kn));
+#pragma unroll
+    for (int p = 0; p < 8; ++p) bn[p] = load_frag<T>((const char*)(brow[p] + kn));
+#pragma unroll
+    for (int p = 0; p < 8; ++p) mfma_frag(acc[p], af, bf[p]);
+    af = an;
+#pragma unroll
+    for (int p = 0; p < 8; ++p) bf[p] = bn[p];
+  }
+  const int co = wave * 16 + 4 * g;
+  float bias[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = a.bias[co + i];
+#pragma unroll
+  for (int p = 0; p < 8; ++p) {
+    const int n = n0 + p * 16 + (lane & 15);
+    if (n >= a.N) continue;
+    *(f32x4*)(a.skip + ((size_t)b * a.N + n) * DW_C + co) =
+        f32x4{acc[p][0] + bias[0], acc[p][1] + bias[1], acc[p][2] + bias[2], acc[p][3] + bias[3]};
+  }
+}
+
+hipError_t launch_dw_skip(int dtype, const DWSkipArgs& a, hipStream_t s) {
+  const dim3 grid((a.N + DW_MS - 1) / DW_MS, a.B);
+  if (dtype == DT_F32) hipLaunchKernelGGL(dw_skip_kernel<float>, grid, dim3(256), 0, s, a);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_skip_kernel<bf16_t>, grid, dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(dw_skip_kernel<f16_t>, grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -9,7 +9,7 @@ struct DWState {
   size_t off_tables = 0, off_sp = 0, off_dstab = 0;
   Arena act;                            // activations of the current (B, F)
   int B = -1, F = -1;
-  size_t off_mid = 0, off_up = 0, off_cond = 0, off_xa = 0, off_xb = 0, off_skip = 0, off_eps = 0, off_dsb = 0;
+  size_t off_mid = 0, off_up = 0, off_cond = 0, off_xa = 0, off_xb = 0, off_skip = 0, off_eps = 0, off_dsb = 0, off_z = 0;
 };
 
 // state-dict shapes of DiffWave (diffwave.py:113-131) without the noise_estimate_model. prefix
@@ -134,6 +134,20 @@ static int dw_upload_weights(sddm_ctx* c) {
     add_t("l" + std::to_string(i) + ".w2", w2);
     add_f32("l" + std::to_string(i) + ".b2", b2);
   }
+  {  // every layer's output_projection side by side: [64][L*64] (k = l*64 + ci), biases summed
+    std::vector<float> wo((size_t)C * d.L * C), bo(C, 0.f);
+    for (int i = 0; i < d.L; ++i) {
+      const std::string p = "residual_layers." + std::to_string(i) + ".";
+      const auto& w = P(p + "output_projection.weight");
+      const auto& bb = P(p + "output_projection.bias");
+      for (int co = 0; co < C; ++co) {
+        for (int ci = 0; ci < C; ++ci) wo[(size_t)co * d.L * C + (size_t)i * C + ci] = w[(size_t)co * C + ci];
+        bo[co] += bb[co];
+      }
+    }
+    add_t("skip.w", wo);
+    add_f32("skip.b", bo);
+  }
   add_f32("emb.pw", pw);
   add_f32("emb.pb", pb);
   add_t("cond.w", cw);
@@ -167,6 +181,7 @@ static int dw_prepare(sddm_ctx* c, int B, int F) {
   d.off_xa = A.reserve(es * (size_t)B * N * d.C);
   d.off_xb = A.reserve(es * (size_t)B * N * d.C);
   d.off_skip = A.reserve(sizeof(float) * (size_t)B * N * d.C);
+  d.off_z = A.reserve(es * (size_t)B * N * d.L * d.C);
   d.off_eps = A.reserve(sizeof(float) * (size_t)B * N);
   d.off_dsb = A.reserve(sizeof(float) * (size_t)B * d.L * d.C);
   SDDM_HIP_CHECK(A.commit());
@@ -222,7 +237,7 @@ static int dw_network(sddm_ctx* c, const float* audio, int B, int F, const float
     DWLayerArgs a{};
     a.x_in = d.act.base + (i % 2 ? d.off_xb : d.off_xa);
     a.x_out = d.act.base + (i % 2 ? d.off_xa : d.off_xb);
-    a.skip = d.act.at<float>(d.off_skip); a.first = i == 0;
+    a.z = d.act.base + d.off_z; a.first = i == 0;
     a.cond = d.act.base + d.off_cond; a.layer = i; a.L = d.L;
     a.ds = ds; a.t_dev = t_dev; a.ds_per_b = ds_per_b;
     a.w1 = W.base + d.woff.at("l" + std::to_string(i) + ".w1"); a.b1 = W.at<float>(d.woff.at("l" + std::to_string(i) + ".b1"));
@@ -230,6 +245,10 @@ static int dw_network(sddm_ctx* c, const float* audio, int B, int F, const float
     a.dil = 1 << (i % d.cycle); a.N = N; a.B = B;
     SDDM_HIP_CHECK(launch_dw_layer(c->dtype, a, s));
   }
+  DWSkipArgs sk{};
+  sk.z = d.act.base + d.off_z; sk.w = W.base + d.woff.at("skip.w"); sk.bias = W.at<float>(d.woff.at("skip.b"));
+  sk.skip = d.act.at<float>(d.off_skip); sk.B = B; sk.N = N; sk.L = d.L;
+  SDDM_HIP_CHECK(launch_dw_skip(c->dtype, sk, s));
   DWOutArgs o{};
   o.skip = d.act.at<float>(d.off_skip);
   o.wsp = W.at<float>(d.woff.at("sp.w")); o.bsp = W.at<float>(d.woff.at("sp.b"));

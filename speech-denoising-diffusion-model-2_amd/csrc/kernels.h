@@ -146,15 +146,19 @@ hipError_t launch_dw_cond(int dtype, const DWCondArgs& a, hipStream_t s);
 struct DWInArgs { const float* audio; const float* w; const float* b; void* x; int64_t total; int* t_dev; };
 hipError_t launch_dw_input(int dtype, const DWInArgs& a, hipStream_t s);
 struct DWLayerArgs {
-  const void* x_in; void* x_out; float* skip; int first;
+  const void* x_in; void* x_out; void* z; int first;   // z: gated activations [B][N][L][64] (T)
   const void* cond; int layer, L;
   const float* ds; const int* t_dev; int ds_per_b;   // [rows][L][64]
   const void* w1; const float* b1;                   // dilated conv [128][3*64] (k = tap*64 + ci), bias [128]
-  const void* w2; const float* b2;                   // [output_residual; output_projection] [128][64], [128]
+  const void* w2; const float* b2;                   // output_residual [64][64] (rows 0-63 used), bias
   int dil, N, B;
 };
 hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s);
 size_t dw_layer_lds_bytes(int dtype);
+struct DWSkipArgs {           // skip[b][n][64] = Wo_all [64][L*64] z[b][n][L*64] + bias_sum (fp32 out)
+  const void* z; const void* w; const float* bias; float* skip; int B, N, L;
+};
+hipError_t launch_dw_skip(int dtype, const DWSkipArgs& a, hipStream_t s);
 struct DWOutArgs {
   const float* skip; const float* wsp; const float* bsp; const float* wop; const float* bop;
   float sqrt_layers; float* eps; int64_t total;
