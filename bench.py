@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--workload", default="unet", choices=["unet", "diffwave", "wavegrad"])
+    ap.add_argument("--num-samples", type=int, default=None,
+                    help="UNet chunk length (config #5: 32832 = 512 frames); default config_unet.json's 16448")
     import sys as _sys
     args = ap.parse_args()
     args.batch_set = any(a.startswith("--batch") for a in _sys.argv[1:])
@@ -220,6 +222,8 @@ def main():
 
     cfg = read_json(os.path.join(PKG, "configs", "config_unet_bench.json"))
     cfg["diffusion"]["args"]["n_timestep"] = args.timesteps
+    if args.num_samples:
+        cfg["num_samples"] = args.num_samples
     config = ConfigParser(cfg)
     N = config["num_samples"]
     T = args.timesteps
@@ -280,7 +284,7 @@ def main():
             # (tools/gpu_traffic.sh + tools/traffic.py; counters cannot be read from inside this run)
             traffic, tsrc = None, None
             tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_traffic.json")
-            if os.path.exists(tf):
+            if os.path.exists(tf) and (N, B, args.dtype, T) == (16448, 16, "bf16", 1000):   # the PMC workload
                 with open(tf) as fh:
                     traffic = round(json.load(fh)["bytes_per_launch"])
                 tsrc = "profiles/hbm_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same workload)"
@@ -307,7 +311,7 @@ def main():
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
                 "data": "synthetic (harmonic speech + gaussian noise, 16 kHz), random-init weights",
                 "config": {"workload": f"UNetModified2 config_unet.json, linear 1e-6..1e-3, T={T}, "
-                                       f"{B}x16448-sample chunks per GPU, condition_in",
+                                       f"{B}x{N}-sample chunks per GPU, condition_in",
                            "model": "UNetModified2", "global_batch": B * world, "seq_len": N,
                            "timesteps": T, "parallelism": f"dp{world}"},
                 "roofline": roofline, "cpu_baseline": cpu}

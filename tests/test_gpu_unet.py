@@ -156,3 +156,29 @@ def test_transitions_match_reference(torch_cuda):
             worst = max(worst, d)
             assert d <= 2e-6, (key, d)
     print("worst transition diff", worst)
+
+
+@pytest.mark.parametrize("dtype,tol", [("float32", 1e-4), ("float16", 5e-3)])
+def test_unet_forward_config5_geometry(torch_cuda, dtype, tol):
+    """BASELINE config #5 shape: 2.05 s chunks (N=32832, 512 frames; every level twice as tall)
+    in fp16 storage with fp32 GroupNorm statistics, against the numpy oracle, B=4 with mixed
+    noise levels (parity unpinned by a reference golden at this length: oracle only)."""
+    from oracle import unet
+    from sddm_hip.synth import noisy_speech
+    from _helpers import unet_arch
+    N, B = 32832, 4
+    rng = np.random.default_rng(12)
+    cond = noisy_speech(B, N, seed=12)
+    x_t = (0.7 * cond + 0.7 * rng.standard_normal(cond.shape)).astype(np.float32)
+    nl = np.array([0.99, 0.7, 0.4, 0.1], dtype=np.float32).reshape(B, 1, 1)
+    ref = unet.forward(unet_params(N), unet_arch(N), cond, x_t, nl.reshape(-1))
+    dev = torch_cuda.device("cuda", 0)
+    eps = torch_cuda.full((B, 1, N), float("nan"), device=dev)
+    make_ctx(N, dtype).network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
+                                       torch_cuda.from_numpy(nl).to(dev), eps)
+    torch_cuda.cuda.synchronize()
+    got = eps.cpu().numpy()
+    assert np.isfinite(got).all()
+    err = rms(got, ref)
+    print(f"{dtype} forward N={N}: rms err {err:.3e}")
+    assert err <= tol
