@@ -192,17 +192,20 @@ __global__ __launch_bounds__(256) void wg_conv_kernel(WGConvArgs a) {
 // leaky applied here, once per element) and (b) the weights of all KT taps for its 128 channels;
 // every tap then reads its B fragments from the slab at a row offset of tap * dil.  The next
 // chunk's global loads are issued before the current chunk's MFMAs.
-constexpr int WGL_MC = 128, WGL_MT = 128, WGL_HALO = 8;
+constexpr int WGL_MC = 128, WGL_HALO = 8;
 
-template <typename T, int PRE, int KT>
-__global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
+// TW = waves along time: block = 2 x TW waves = 128 channels x 64 TW positions (TW = 4 halves the
+// per-position weight traffic from L2 on the long levels)
+template <typename T, int PRE, int KT, int TW>
+__global__ __launch_bounds__(128 * TW) void wg_conv_lds_kernel(WGConvArgs a) {
 #pragma clang fp contract(off)
+  constexpr int NT = 128 * TW, WGL_MT = 64 * TW;
   constexpr int ES = (int)sizeof(T), UE = 16 / ES;         // elements per 16-byte unit
   constexpr int UPR = 32 / UE;                              // units per 32-channel row
   constexpr int RS = UPR * 16 + 16;                         // padded LDS row stride (bytes)
   constexpr int SROWS = WGL_MT + 2 * WGL_HALO;
   constexpr int NBU = SROWS * UPR, NAU = KT * WGL_MC * UPR;
-  constexpr int PB = (NBU + 255) / 256, PA = (NAU + 255) / 256;
+  constexpr int PB = (NBU + NT - 1) / NT, PA = (NAU + NT - 1) / NT;
   __shared__ __attribute__((aligned(16))) char lds[(SROWS + KT * WGL_MC) * RS];
   char* slab = lds;
   char* wl = lds + SROWS * RS;
@@ -221,7 +224,7 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
   auto gload = [&](int c0) {
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
-      const int u = tid + j * 256;
+      const int u = tid + j * NT;
       const int r = u / UPR, q = u - r * UPR;
       const int tp = t0 - H + r;
       breg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -235,7 +238,7 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
-      const int u = tid + j * 256;
+      const int u = tid + j * NT;
       const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
       if (u < NAU) areg[j] = *(const f32x4*)(W + ((size_t)(cob + co) * KT + k) * Cin + c0 + q * UE);
     }
@@ -243,7 +246,7 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
   auto lstore = [&]() {
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
-      const int u = tid + j * 256;
+      const int u = tid + j * NT;
       if (u >= rows * UPR) continue;
       const int r = u / UPR, q = u - r * UPR;
       f32x4 v = breg[j];
@@ -266,7 +269,7 @@ __global__ __launch_bounds__(256) void wg_conv_lds_kernel(WGConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
-      const int u = tid + j * 256;
+      const int u = tid + j * NT;
       if (u >= NAU) continue;
       const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
       *(f32x4*)(wl + (k * WGL_MC + co) * RS + q * 16) = areg[j];
@@ -337,19 +340,27 @@ bool wg_conv_uses_lds(const WGConvArgs& a) {
          (!off && a.Cout % WGL_MC == 0 && !a.out_f32 && a.K == 1 && a.pre != 2);
 }
 
+template <typename T, int PRE, int TW>
+static void wg_conv_lds_dispatch(const WGConvArgs& a, hipStream_t s) {
+  const dim3 grid((a.Tc + 64 * TW - 1) / (64 * TW), a.Cout / WGL_MC, a.B);
+  if (a.K == 1) hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE == 2 ? 0 : PRE, 1, TW>), grid, dim3(128 * TW), 0, s, a);
+  else hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3, TW>), grid, dim3(128 * TW), 0, s, a);
+}
+
 template <typename T, int PRE>
-static void wg_conv_lds_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
-  if (a.K == 1) hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE == 2 ? 0 : PRE, 1>), grid, dim3(256), 0, s, a);
-  else hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3>), grid, dim3(256), 0, s, a);
+static void wg_conv_lds_pick(const WGConvArgs& a, hipStream_t s) {
+  static const int tw_env = std::getenv("SDDM_WG_TW") ? std::atoi(std::getenv("SDDM_WG_TW")) : 0;
+  const bool wide = tw_env == 4;   // 256-position tiles: measured no faster (165 vs 169 audio-s/s)
+  if (wide) wg_conv_lds_dispatch<T, PRE, 4>(a, s);
+  else wg_conv_lds_dispatch<T, PRE, 2>(a, s);
 }
 
 template <typename T>
 static void wg_conv_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
   if (wg_conv_uses_lds(a)) {
-    const dim3 g2((a.Tc + WGL_MT - 1) / WGL_MT, a.Cout / WGL_MC, a.B);
-    if (a.pre == 0) wg_conv_lds_dispatch<T, 0>(a, g2, s);
-    else if (a.pre == 1) wg_conv_lds_dispatch<T, 1>(a, g2, s);
-    else wg_conv_lds_dispatch<T, 2>(a, g2, s);
+    if (a.pre == 0) wg_conv_lds_pick<T, 0>(a, s);
+    else if (a.pre == 1) wg_conv_lds_pick<T, 1>(a, s);
+    else wg_conv_lds_pick<T, 2>(a, s);
     return;
   }
   if (a.pre == 0) hipLaunchKernelGGL((wg_conv_kernel<T, 0>), grid, dim3(256), 0, s, a);
