@@ -356,46 +356,61 @@ hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
 // activation z_l [B][N][L][64] in one GEMM instead of a per-layer fp32 read-modify-write.
 template <typename T>
 __global__ __launch_bounds__(256) void dw_skip_kernel(DWSkipArgs a) {
+  // block = 256 samples; wave w owns samples [64 w, +64) x all 64 channels (4 x 4 MFMA tiles), so
+  // every z fragment is read from HBM exactly once and the weight fragments come from L2
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int n0 = blockIdx.x * DW_MS, b = blockIdx.y, K = a.L * DW_C;
-  const T* arow = (const T*)a.w + (size_t)(wave * 16 + (lane & 15)) * K + g * 8;
+  const int n0 = blockIdx.x * 256 + wave * 64, b = blockIdx.y, K = a.L * DW_C;
   const T* Z = (const T*)a.z + (size_t)b * a.N * K;
-  const T* brow[8];
+  const T* arow[4];
+  const T* brow[4];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) brow[p] = Z + (size_t)min(n0 + p * 16 + (lane & 15), a.N - 1) * K + g * 8;
-  f32x4 acc[8];
+  for (int c = 0; c < 4; ++c) arow[c] = (const T*)a.w + (size_t)(c * 16 + (lane & 15)) * K + g * 8;
 #pragma unroll
-  for (int p = 0; p < 8; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
-  Frag<T> af = load_frag<T>((const char*)arow), bf[8];
+  for (int p = 0; p < 4; ++p) brow[p] = Z + (size_t)min(n0 + p * 16 + (lane & 15), a.N - 1) * K + g * 8;
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) bf[p] = load_frag<T>((const char*)brow[p]);
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag<T> af[4], bf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) af[c] = load_frag<T>((const char*)arow[c]);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) bf[p] = load_frag<T>((const char*)brow[p]);
   for (int k = 0; k < K; k += 32) {
-    Frag<T> an, bn[8];
     const int kn = k + 32 < K ? k + 32 : k;
-    an = load_frag<T>((const char*)(arow + kn));
+    Frag<T> an[4], bn[4];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) bn[p] = load_frag<T>((const char*)(brow[p] + kn));
+    for (int c = 0; c < 4; ++c) an[c] = load_frag<T>((const char*)(arow[c] + kn));
 #pragma unroll
-    for (int p = 0; p < 8; ++p) mfma_frag(acc[p], af, bf[p]);
-    af = an;
+    for (int p = 0; p < 4; ++p) bn[p] = load_frag<T>((const char*)(brow[p] + kn));
 #pragma unroll
-    for (int p = 0; p < 8; ++p) bf[p] = bn[p];
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) mfma_frag(acc[c][p], af[c], bf[p]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) af[c] = an[c];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) bf[p] = bn[p];
   }
-  const int co = wave * 16 + 4 * g;
-  float bias[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) bias[i] = a.bias[co + i];
+  for (int c = 0; c < 4; ++c) {
+    const int co = c * 16 + 4 * g;
+    float bias[4];
 #pragma unroll
-  for (int p = 0; p < 8; ++p) {
-    const int n = n0 + p * 16 + (lane & 15);
-    if (n >= a.N) continue;
-    *(f32x4*)(a.skip + ((size_t)b * a.N + n) * DW_C + co) =
-        f32x4{acc[p][0] + bias[0], acc[p][1] + bias[1], acc[p][2] + bias[2], acc[p][3] + bias[3]};
+    for (int i = 0; i < 4; ++i) bias[i] = a.bias[co + i];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int n = n0 + p * 16 + (lane & 15);
+      if (n >= a.N) continue;
+      *(f32x4*)(a.skip + ((size_t)b * a.N + n) * DW_C + co) =
+          f32x4{acc[c][p][0] + bias[0], acc[c][p][1] + bias[1], acc[c][p][2] + bias[2], acc[c][p][3] + bias[3]};
+    }
   }
 }
 
 hipError_t launch_dw_skip(int dtype, const DWSkipArgs& a, hipStream_t s) {
-  const dim3 grid((a.N + DW_MS - 1) / DW_MS, a.B);
+  const dim3 grid((a.N + 255) / 256, a.B);
   if (dtype == DT_F32) hipLaunchKernelGGL(dw_skip_kernel<float>, grid, dim3(256), 0, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_skip_kernel<bf16_t>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(dw_skip_kernel<f16_t>, grid, dim3(256), 0, s, a);
