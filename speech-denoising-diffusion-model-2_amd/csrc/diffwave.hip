@@ -210,7 +210,7 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
   constexpr int PB = 64 / UPS;                    // samples per 64-unit staging group
   constexpr int PLANE = DW_MS * 16;               // bytes per plane (2 KB, = 0 mod 256)
   constexpr int NU = 3 * DW_MS * UPS;             // staged units
-  constexpr int MAXU = 4;
+  constexpr int MAXU = 12;
   typedef T vec4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* yin = smem;                               // [3 taps][UPS][128 samples][16 B]
