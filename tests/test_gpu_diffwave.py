@@ -55,3 +55,17 @@ def test_diffwave_rejects_bad_geometry(torch_cuda):
     spec = torch.rand(1, 513, 2, device="cuda")
     with pytest.raises(Exception):
         n(spec, torch.zeros(1, 1, 500, device="cuda"), torch.ones(1, 1, 1, device="cuda"))
+
+
+def test_diffwave_row_sharding_is_bit_identical(torch_cuda):
+    """Rows sampled in two shards (row_offset) equal the rows of one batch."""
+    import model.diffusion as D
+    import model.model as M
+    d = D.GaussianDiffusion("linear", 3, 1e-4, 0.05, device="cuda")
+    m = M.SDDM_spectrogram(d, _net("bfloat16"), hop_samples=256, noise_condition="time_step",
+                           compute_dtype="bfloat16").cuda()
+    spec = torch.rand(4, 513, 4, generator=torch.Generator().manual_seed(2)).cuda()
+    full = m.infer(spec, seed=5)
+    a = m.infer(spec[:2].contiguous(), seed=5, row_offset=0)
+    b = m.infer(spec[2:].contiguous(), seed=5, row_offset=2)
+    assert torch.equal(full, torch.cat([a, b]))

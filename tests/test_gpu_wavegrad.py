@@ -80,3 +80,16 @@ def test_wavegrad_rejects_bad_geometry(torch_cuda):
     spec = torch.rand(1, 128, 2, device="cuda")
     with pytest.raises(Exception):
         n(spec, torch.zeros(1, 500, device="cuda"), torch.ones(1, device="cuda"))
+
+
+def test_wavegrad_single_clip_squeezes_like_reference(torch_cuda):
+    """wavegrad.py:179 returns torch.squeeze(output): a single clip comes back as [N]."""
+    from oracle import wavegrad as wg
+    rng = np.random.default_rng(4)
+    spec = rng.uniform(0, 1, (1, 128, 3)).astype(np.float32)
+    audio = rng.standard_normal((1, 900)).astype(np.float32)
+    nl = np.array([0.5], dtype=np.float32)
+    out = _net()(*(torch.from_numpy(x).cuda() for x in (spec, audio, nl)))
+    assert tuple(out.shape) == (900,)
+    ref = wg.forward(wavegrad_params(), spec, audio, nl)[0]
+    assert rms(out.cpu().numpy(), ref) <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref ** 2))))
