@@ -286,6 +286,10 @@ struct sddm_ctx {
   // SDDM_spectrogram + DiffWave
   std::shared_ptr<DWState> dws;
   std::shared_ptr<WGState> wgs;
+  // measured conv_deep tiles per layer name: (pixels per block, waves); valid for one lane batch /
+  // dtype / num_samples (sddm_set_conv_tuning)
+  std::map<std::string, std::pair<int, int>> deep_tune;
+  int tune_B = -1, tune_dtype = -1, tune_N = -1;
   int hop_samples = 256;
 
   const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
@@ -437,7 +441,7 @@ struct ConvChoice {
 // (256 CUs x 2 blocks at 4 waves, x 1 block at 8 waves); among equal round counts 8 waves (the
 // K split 8 ways, weights resident) and then the smaller tile (less work per block) win.
 // SDDM_DEEP_CFG=mt:nw forces one configuration wherever it fits (experiments).
-static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch) {
+static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int want_mt = 0, int want_nw = 0) {
   const int nz = a.Cout / 32;
   static int force_mt = -1, force_nw = -1;
   if (force_mt < 0) {
@@ -462,8 +466,9 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch) {
   }
   if (cs.empty()) return false;
   const Cand* pick = nullptr;
+  const int fm = want_mt ? want_mt : force_mt, fn = want_mt ? want_nw : force_nw;
   for (const Cand& c : cs)
-    if (c.mt == force_mt && c.nw == force_nw) pick = &c;
+    if (c.mt == fm && c.nw == fn) pick = &c;
   if (!pick) {
     pick = &cs[0];
     for (const Cand& c : cs) {
@@ -478,7 +483,7 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch) {
 }
 
 static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
-                        ConvChoice& ch) {
+                        ConvChoice& ch, int want_mt = 0, int want_nw = 0) {
   ConvArgs a{};
   a.CA = Cin; a.CB = 0; a.RCA = RC; a.RCB = 0; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.upsample = up ? 1 : 0;
@@ -511,7 +516,7 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
       }
     }
   }
-  return choose_deep(dt, B, a, s2, ch);
+  return choose_deep(dt, B, a, s2, ch, want_mt, want_nw);
 }
 
 static int build_lane(sddm_ctx* c, Lane& L) {
@@ -558,8 +563,17 @@ static int build_lane(sddm_ctx* c, Lane& L) {
     ConvChoice ch;
   };
   std::vector<Step> prog;
-  auto pick = [&](int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up, ConvChoice& ch) {
-    return choose_conv(dt, B, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch);
+  // measured per-layer deep tiles (sddm_set_conv_tuning) apply when they were measured for this
+  // lane batch, dtype and length; otherwise the round-count heuristic of choose_deep decides
+  const bool tuned = c->tune_B == B && c->tune_dtype == dt && c->tune_N == N;
+  auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
+                  ConvChoice& ch) {
+    int wm = 0, wn = 0;
+    if (tuned) {
+      auto it = c->deep_tune.find(name);
+      if (it != c->deep_tune.end()) { wm = it->second.first; wn = it->second.second; }
+    }
+    return choose_conv(dt, B, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn);
   };
   const int TRin = 512 / W;
   if (u.inner != 32 || 512 % W || F % TRin || (TRin + 1) * S + W + 2 > 1024)
@@ -570,8 +584,8 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   auto res_block = [&](const std::string& n, int xa, int xb, int cin, int cout) -> int {
     const int H = tres[xa].H, Wd = tres[xa].W;
     ConvChoice c1, c2;
-    if (!pick(cin, 0, 0, H, Wd, cout, false, false, c1)) return -1;
-    if (!pick(cout, cin, cin != cout ? 2 : 1, H, Wd, cout, false, false, c2)) return -1;
+    if (!pick(n + ".block1", cin, 0, 0, H, Wd, cout, false, false, c1)) return -1;
+    if (!pick(n + ".block2", cout, cin, cin != cout ? 2 : 1, H, Wd, cout, false, false, c2)) return -1;
     const int g1 = new_gn(xa, xb, n + ".block1");
     const int h = new_tensor(cout, H, Wd, c1.n_tiles, c1.TR * c1.TW);
     { Step st; st.type = ST_CONV; st.w = n + ".block1"; st.rb = n; st.srcA = xa; st.srcB = xb; st.gn = g1;
@@ -594,7 +608,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       if (tres[cur].H % 2 || tres[cur].W % 2) FAIL(SDDM_ERR_SHAPE, "odd size before %s", L.name.c_str());
       const int H = tres[cur].H / 2, Wd = tres[cur].W / 2;
       ConvChoice ch;
-      if (!pick(tres[cur].C, 0, 0, H, Wd, L.cout, true, false, ch)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+      if (!pick(L.name, tres[cur].C, 0, 0, H, Wd, L.cout, true, false, ch)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
       const int o = new_tensor(L.cout, H, Wd, ch.n_tiles, ch.TR * ch.TW);
       Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.s2 = 1; st.cout = L.cout; st.ch = ch;
       prog.push_back(st);
@@ -618,7 +632,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
     } else {
       const int H = tres[cur].H * 2, Wd = tres[cur].W * 2;
       ConvChoice ch;
-      if (!pick(tres[cur].C, 0, 0, H, Wd, L.cout, false, true, ch)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
+      if (!pick(L.name, tres[cur].C, 0, 0, H, Wd, L.cout, false, true, ch)) FAIL(SDDM_ERR_SHAPE, "no tile for %s", L.name.c_str());
       const int o = new_tensor(L.cout, H, Wd, ch.n_tiles, ch.TR * ch.TW);
       Step st; st.type = ST_CONV; st.w = L.name; st.srcA = cur; st.out = o; st.up = 1; st.cout = L.cout; st.ch = ch;
       prog.push_back(st);
@@ -1314,6 +1328,29 @@ int sddm_q_sample(sddm_ctx* c, int mode, const float* x0, const float* y, const 
   a.sab = c->dtab(3); a.alpha_bar = c->dtab(2); a.m = c->dtab(8); a.sqrt_delta = c->dtab(9);
   a.x_t = x_t; a.combined = combined; a.s_out = s_out; a.level_out = level_out; a.B = B; a.N = N;
   SDDM_HIP_CHECK(launch_q_sample(a, (hipStream_t)stream));
+  return SDDM_OK;
+}
+
+int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
+  if (!c || !json) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
+  Json j;
+  try {
+    j = Json::parse(json);
+  } catch (const std::exception& e) {
+    FAIL(SDDM_ERR_INVALID_ARG, "tuning JSON: %s", e.what());
+  }
+  const std::string dts = j.string("dtype", "");
+  const int dt = dts == "float32" ? DT_F32 : dts == "bfloat16" ? DT_BF16 : dts == "float16" ? DT_F16 : -1;
+  c->deep_tune.clear();
+  for (const auto& kv : j.at("deep").obj) {
+    if (kv.second.kind != Json::ARR || kv.second.arr.size() != 2) FAIL(SDDM_ERR_INVALID_ARG, "deep.%s: [mt, nw]", kv.first.c_str());
+    c->deep_tune[kv.first] = {(int)kv.second.arr[0].num, (int)kv.second.arr[1].num};
+  }
+  c->tune_B = (int)j.number("lane_batch", -1);
+  c->tune_dtype = dt;
+  c->tune_N = (int)j.number("num_samples", -1);
+  c->plan_B = -1;                                   // re-plan on the next call
+  c->lanes.clear();
   return SDDM_OK;
 }
 

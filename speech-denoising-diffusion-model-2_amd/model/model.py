@@ -10,12 +10,15 @@ returns x_0.  Extra keyword arguments (all optional, defaults keep the reference
               same noise whatever rank samples them)
   compute_dtype (constructor / attribute): 'float32' (parity, default), 'bfloat16', 'float16'
 """
+import os
+
 import torch
 from torch import nn
 
 import sddm_hip
 from .diffusion import GaussianDiffusion, _seed_from_torch
 
+_TUNING = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "conv_tuning.json")
 _P_TRANSITIONS = ("original", "supportive", "sr3", "conditional", "condition_in")
 
 
@@ -61,6 +64,9 @@ class SDDM(nn.Module):
         if self._ctx is None or self._ctx_key != key:
             ctx = sddm_hip.Context(self.library_config(), device.index or 0, self.compute_dtype)
             ctx.load_state_dict(sd)
+            if os.path.exists(_TUNING):           # measured conv tiles (tools/tune_deep.py)
+                with open(_TUNING) as f:
+                    ctx.set_conv_tuning(f.read())
             self._ctx, self._ctx_key = ctx, key
         return self._ctx
 

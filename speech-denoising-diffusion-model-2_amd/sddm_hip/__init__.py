@@ -25,7 +25,7 @@ TABLE_NAMES = ("betas", "alphas", "alpha_bar", "sqrt_alpha_bar", "predicted_nois
 EXPORTS = ("sddm_abi_version", "sddm_last_error", "sddm_create", "sddm_destroy", "sddm_configure",
            "sddm_load_param", "sddm_missing_params", "sddm_sample", "sddm_sample_continuous",
            "sddm_network_forward",
-           "sddm_transition", "sddm_q_sample", "sddm_log_spectrogram", "sddm_initial_state", "sddm_schedule", "sddm_profile_enable",
+           "sddm_transition", "sddm_q_sample", "sddm_log_spectrogram", "sddm_set_conv_tuning", "sddm_initial_state", "sddm_schedule", "sddm_profile_enable",
            "sddm_profile_read", "sddm_profile_ops")
 
 _lib = None
@@ -54,6 +54,7 @@ def lib():
         L.sddm_transition.argtypes = [vp, c_int, vp, vp, vp, c_int, i64, i64, u64, i64, vp, vp]
         L.sddm_q_sample.argtypes = [vp, c_int, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp]
         L.sddm_log_spectrogram.argtypes = [vp, i64, i64, c_int, c_int, vp, vp, c_int, vp, vp]
+        L.sddm_set_conv_tuning.argtypes = [vp, ctypes.c_char_p]
         L.sddm_initial_state.argtypes = [vp, c_int, vp, i64, i64, u64, i64, vp, vp]
         L.sddm_schedule.argtypes = [ctypes.c_char_p, c_int, ctypes.c_double, ctypes.c_double, vp]
         L.sddm_profile_enable.argtypes = [vp, c_int]
@@ -166,6 +167,12 @@ class Context:
         check(lib().sddm_transition(self._h, int(mode), _ptr(x_t), _ptr(eps), _ptr(cond), int(t), B, N,
                                     int(seed) & (2 ** 64 - 1), int(row_offset), _ptr(out),
                                     _stream(torch, x_t.device)))
+
+    def set_conv_tuning(self, table):
+        """Per-layer conv tiles measured by tools/tune_deep.py (dict or JSON text)."""
+        import json as _json
+        text = table if isinstance(table, str) else _json.dumps(table)
+        check(lib().sddm_set_conv_tuning(self._h, text.encode()))
 
     def q_sample(self, mode, x0, y, noise, t, r, x_t, combined, s_out, level_out):
         import torch

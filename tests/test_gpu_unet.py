@@ -59,10 +59,12 @@ def test_unet_forward_reduced_precision(torch_cuda, dtype, tol):
     assert err <= tol
 
 
-@pytest.mark.parametrize("dtype,tol", [("float32", 1e-4), ("bfloat16", 2.5e-2)])
-def test_unet_forward_bench_batch(torch_cuda, dtype, tol):
+@pytest.mark.parametrize("dtype,tol,tuned", [("float32", 1e-4, False), ("bfloat16", 2.5e-2, False),
+                                            ("bfloat16", 2.5e-2, True)])
+def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     """B=16 x N=16448 (the bench shape): the kernel/tile configurations picked for a full batch
-    (not the B=1 ones) reproduce the reference on every row; rows use mixed noise levels."""
+    (not the B=1 ones) -- and per-layer tiles set through sddm_set_conv_tuning -- reproduce the
+    reference on every row; rows use mixed noise levels."""
     N, B = 16448, 16
     fw = golden("unet_forward.npz")
     dev = torch_cuda.device("cuda", 0)
@@ -70,6 +72,10 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol):
     x_t = np.repeat(fw[f"fw/{N}/x_t"], B, axis=0)
     nl = np.repeat(fw[f"fw/{N}/noise_level"], B, axis=0)
     ctx = make_ctx(N, dtype)
+    if tuned:     # sddm_set_conv_tuning: per-layer conv_deep tiles other than the heuristic's
+        ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N,
+                             "deep": {"downs.6": [64, 4], "downs.8": [32, 8], "mid.0.block1": [32, 8],
+                                      "ups.5.block1": [64, 4], "ups.7": [128, 4]}})
     eps = torch_cuda.full((B, 1, N), float("nan"), device=dev)
     ctx.network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
                         torch_cuda.from_numpy(nl).to(dev), eps)
