@@ -355,8 +355,56 @@ static void wg_conv_lds_pick(const WGConvArgs& a, hipStream_t s) {
   else wg_conv_lds_dispatch<T, PRE, 2>(a, s);
 }
 
+// last_conv (Conv1d(128, 1, 3, padding=1), wavegrad.py:164, 178): an MFMA tile would be 1/128
+// useful, so each 16-lane group reads one position's 128 channels as 16 contiguous 16-byte units
+// (coalesced), forms the three tap dot products d_k[p] = w_k . x[p] with a 16-lane shuffle
+// reduction, parks them in LDS, and out[t] = bias + d_0[t-1] + d_1[t] + d_2[t+1].
+constexpr int WG1_MT = 128;
+template <typename T>
+__global__ __launch_bounds__(256) void wg_last_kernel(WGConvArgs a) {
+#pragma clang fp contract(off)
+  __shared__ float d[3][WG1_MT + 2];
+  const int tid = threadIdx.x, grp = tid >> 4, l = tid & 15;
+  const int b = blockIdx.y, t0 = blockIdx.x * WG1_MT, Tc = a.Tc;
+  const T* src_b = (const T*)a.src + (size_t)b * a.src_T * a.src_C;
+  float w[3][8];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) load8<T>((const T*)a.w + k * 128 + l * 8, w[k]);
+  for (int r = grp; r < WG1_MT + 2; r += 16) {      // positions t0 - 1 .. t0 + WG1_MT
+    const int p = t0 - 1 + r;
+    float acc[3] = {0.f, 0.f, 0.f};
+    if (p >= 0 && p < Tc) {
+      float v[8];
+      load8<T>(src_b + (size_t)p * a.src_C + l * 8, v);
+#pragma unroll
+      for (int k = 0; k < 3; ++k)
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[k] += w[k][e] * v[e];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) acc[k] += __shfl_xor(acc[k], o, 16);
+    if (l == 0) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) d[k][r] = acc[k];
+    }
+  }
+  __syncthreads();
+  if (tid < WG1_MT) {
+    const int t = t0 + tid;
+    if (t < Tc) ((float*)a.out)[(size_t)b * Tc + t] = a.bias[0] + d[0][tid] + d[1][tid + 1] + d[2][tid + 2];
+  }
+}
+
 template <typename T>
 static void wg_conv_dispatch(const WGConvArgs& a, dim3 grid, hipStream_t s) {
+  static const bool no_last = std::getenv("SDDM_WG_NO_LAST") != nullptr;
+  if (!no_last && a.Cout == 1 && a.out_f32 && a.K == 3 && a.dil == 1 && a.Cin == 128 && a.pre == 0 &&
+      a.map == WG_MAP_ID && !a.res && a.post == 0) {
+    hipLaunchKernelGGL(wg_last_kernel<T>, dim3((a.Tc + WG1_MT - 1) / WG1_MT, a.B), dim3(256), 0, s, a);
+    return;
+  }
   if (wg_conv_uses_lds(a)) {
     if (a.pre == 0) wg_conv_lds_pick<T, 0>(a, s);
     else if (a.pre == 1) wg_conv_lds_pick<T, 1>(a, s);
