@@ -4,7 +4,7 @@
 // contiguous 16-byte units and every MFMA operand fragment is one vector load.  Per sampling
 // call the step-invariant work runs once: the SpectrogramUpsampler (2 ConvTranspose2d passes,
 // diffwave.py:48-61) and the conditioner projections of all residual layers
-// (conditioner_projection, diffwave.py:93), kept as cond[B][N][L][2C]; the noise-step
+// (conditioner_projection, diffwave.py:93), kept layer-major as cond[L][B][N][2C]; the noise-step
 // embedding MLP and every layer's diffusion_projection are tabulated for all t (one row per t).
 // Per reverse step: input projection, one fused kernel per residual layer, one output kernel.
 //
@@ -122,7 +122,7 @@ hipError_t launch_dw_upsample(int dtype, const DWUpArgs& a, hipStream_t s) {
 }
 
 // ---------------- conditioner projections of all layers (step-invariant GEMM) ----------------
-// cond[b][n][l][co] = sum_k Wc[l][co][k] spec[b][n][k] + bc[l][co]; block = 128 samples x 128 co
+// cond[l][b][n][co] = sum_k Wc[l][co][k] spec[b][n][k] + bc[l][co]; block = 128 samples x 128 co
 template <typename T>
 __global__ __launch_bounds__(256) void dw_cond_kernel(DWCondArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void dw_cond_kernel(DWCondArgs a) {
     for (int p = 0; p < 8; ++p) {
       const int n = n0 + p * 16 + (lane & 15);
       if (n >= a.N) continue;
-      store4<T>(out + (((size_t)b * a.N + n) * a.L + l) * 128 + co, acc[c][p][0] + bias[0], acc[c][p][1] + bias[1],
+      store4<T>(out + (((size_t)l * a.B + b) * a.N + n) * 128 + co, acc[c][p][0] + bias[0], acc[c][p][1] + bias[1],
                 acc[c][p][2] + bias[2], acc[c][p][3] + bias[3]);
     }
   }
@@ -254,11 +254,11 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
   // conditioner + bias of this lane's gate / filter rows (issued before GEMM 1, used after it)
   vec4 cnd[2][8];
   {
-    const T* cb = (const T*)a.cond + a.layer * 128;
+    const T* cb = (const T*)a.cond + (size_t)a.layer * a.B * N * 128;   // layer-major: one stream per layer
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       const int n = min(n0 + p * 16 + (lane & 15), N - 1);
-      const T* cp = cb + ((size_t)b * N + n) * a.L * 128;
+      const T* cp = cb + ((size_t)b * N + n) * 128;
       cnd[0][p] = *(const vec4*)(cp + cg);
       cnd[1][p] = *(const vec4*)(cp + cg + 64);
     }

@@ -139,7 +139,7 @@ struct DWUpArgs {             // SpectrogramUpsampler: spec [B][H][F] -> out [B]
   const float* k1; const float* b1; const float* k2; const float* b2;
 };
 hipError_t launch_dw_upsample(int dtype, const DWUpArgs& a, hipStream_t s);
-struct DWCondArgs {           // cond[b][n][l][128] = Wc[l] spec[b][n] + bc[l]
+struct DWCondArgs {           // cond[l][b][n][128] = Wc[l] spec[b][n] + bc[l]
   const void* spec; const void* w; const float* bias; void* out; int B, N, L, Kp;
 };
 hipError_t launch_dw_cond(int dtype, const DWCondArgs& a, hipStream_t s);
