@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
       char* zp = zl + (cg / VE) * PLANE + (p * 16 + (lane & 15)) * 16 + (cg % VE) * ES;
       store4<T>((T*)zp, z[0], z[1], z[2], z[3]);
       const int n = n0 + p * 16 + (lane & 15);      // z of every layer, for the deferred skip GEMM
-      if (n < N) store4<T>((T*)a.z + (((size_t)b * N + n) * a.L + a.layer) * DW_C + cg, z[0], z[1], z[2], z[3]);
+      if (n < N) store4<T>((T*)a.z + (((size_t)a.layer * a.B + b) * N + n) * DW_C + cg, z[0], z[1], z[2], z[3]);
     }
   }
   __syncthreads();
@@ -353,20 +353,21 @@ hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
 
 // ---------------- deferred skip sum: skip[b][n][co] = sum_l Wo_l z_l + sum_l bo_l (K = L x 64) ----------------
 // diffwave.py:104-106, 150-152: every layer's output_projection applied to its stored gated
-// activation z_l [B][N][L][64] in one GEMM instead of a per-layer fp32 read-modify-write.
+// activation z_l (layer-major [L][B][N][64]) in one GEMM instead of a per-layer fp32 read-modify-write.
 template <typename T>
 __global__ __launch_bounds__(256) void dw_skip_kernel(DWSkipArgs a) {
   // block = 256 samples; wave w owns samples [64 w, +64) x all 64 channels (4 x 4 MFMA tiles), so
   // every z fragment is read from HBM exactly once and the weight fragments come from L2
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int n0 = blockIdx.x * 256 + wave * 64, b = blockIdx.y, K = a.L * DW_C;
-  const T* Z = (const T*)a.z + (size_t)b * a.N * K;
+  const size_t LS = (size_t)a.B * a.N * DW_C;        // z is layer-major: [L][B][N][64]
+  const T* Z = (const T*)a.z + (size_t)b * a.N * DW_C;
   const T* arow[4];
   const T* brow[4];
 #pragma unroll
   for (int c = 0; c < 4; ++c) arow[c] = (const T*)a.w + (size_t)(c * 16 + (lane & 15)) * K + g * 8;
 #pragma unroll
-  for (int p = 0; p < 4; ++p) brow[p] = Z + (size_t)min(n0 + p * 16 + (lane & 15), a.N - 1) * K + g * 8;
+  for (int p = 0; p < 4; ++p) brow[p] = Z + (size_t)min(n0 + p * 16 + (lane & 15), a.N - 1) * DW_C + g * 8;
   f32x4 acc[4][4];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(256) void dw_skip_kernel(DWSkipArgs a) {
 #pragma unroll
     for (int c = 0; c < 4; ++c) an[c] = load_frag<T>((const char*)(arow[c] + kn));
 #pragma unroll
-    for (int p = 0; p < 4; ++p) bn[p] = load_frag<T>((const char*)(brow[p] + kn));
+    for (int p = 0; p < 4; ++p) bn[p] = load_frag<T>((const char*)(brow[p] + (size_t)(kn >> 6) * LS + (kn & 63)));
 #pragma unroll
     for (int c = 0; c < 4; ++c)
 #pragma unroll

@@ -146,7 +146,7 @@ hipError_t launch_dw_cond(int dtype, const DWCondArgs& a, hipStream_t s);
 struct DWInArgs { const float* audio; const float* w; const float* b; void* x; int64_t total; int* t_dev; };
 hipError_t launch_dw_input(int dtype, const DWInArgs& a, hipStream_t s);
 struct DWLayerArgs {
-  const void* x_in; void* x_out; void* z; int first;   // z: gated activations [B][N][L][64] (T)
+  const void* x_in; void* x_out; void* z; int first;   // z: gated activations [L][B][N][64] (T)
   const void* cond; int layer, L;
   const float* ds; const int* t_dev; int ds_per_b;   // [rows][L][64]
   const void* w1; const float* b1;                   // dilated conv [128][3*64] (k = tap*64 + ci), bias [128]
