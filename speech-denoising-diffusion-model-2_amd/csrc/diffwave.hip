@@ -209,7 +209,6 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
   constexpr int UPS = DW_C / VE;                  // 16-byte units (planes) per sample and tap
   constexpr int PB = 64 / UPS;                    // samples per 64-unit staging group
   constexpr int PLANE = DW_MS * 16;               // bytes per plane (2 KB, = 0 mod 256)
-  constexpr int NU = 3 * DW_MS * UPS;             // staged units
   constexpr int MAXU = 12;
   typedef T vec4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -224,19 +223,26 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
   const float* ds = a.ds + ((size_t)row * a.L + a.layer) * DW_C;
 
   const int cg = wave * 16 + 4 * g;               // gate row base; filter rows cg + 64
-  // ---- 1. y = x + diffusion projection at the three taps -> LDS ----
-  for (int u0 = 0; u0 < NU; u0 += MAXU * 256) {
+  // ---- 1. y = x + diffusion projection -> LDS ----
+  // dilation <= 64: one window of rows n0 - d .. n0 + 127 + d (the three taps overlap; each x row
+  // is read and transformed once), planes padded to 256 B; larger dilations: three disjoint tap
+  // images of 128 rows
+  const bool win = d <= 64;
+  const int ROWS = win ? (DW_MS + 2 * d + PB - 1) / PB * PB : DW_MS, TAPS = win ? 1 : 3;   // whole staging groups
+  const int PL = win ? (ROWS * 16 + 255) / 256 * 256 : PLANE;
+  const int NUr = TAPS * ROWS * UPS;
+  for (int u0 = 0; u0 < NUr; u0 += MAXU * 256) {
     f32x4 reg[MAXU];
     int dst[MAXU], qv[MAXU];
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
-      const int u = min(u0 + tid + k * 256, NU - 1);
-      const int tap = u / (DW_MS * UPS), r = u - tap * (DW_MS * UPS);
+      const int u = min(u0 + tid + k * 256, NUr - 1);
+      const int tap = u / (ROWS * UPS), r = u - tap * (ROWS * UPS);
       const int grp = r >> 6, j = r & 63, q = j / PB, s = grp * PB + (j % PB);
-      const int n = n0 + s + (tap - 1) * d;
-      const bool ok = n >= 0 && n < N && u0 + tid + k * 256 < NU;
+      const int n = win ? n0 - d + s : n0 + s + (tap - 1) * d;
+      const bool ok = n >= 0 && n < N && u0 + tid + k * 256 < NUr;
       reg[k] = *(const f32x4*)(xin + (size_t)min(max(n, 0), N - 1) * DW_C + q * VE);
-      dst[k] = (u0 + tid + k * 256 < NU) ? ((tap * UPS + q) * PLANE + s * 16) : -1;
+      dst[k] = (u0 + tid + k * 256 < NUr) ? ((tap * UPS + q) * PL + s * 16) : -1;
       qv[k] = ok ? q : -1;
     }
 #pragma unroll
@@ -277,10 +283,11 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
 #pragma unroll
     for (int c = 0; c < 2; ++c)
       af[c] = load_frag<T>((const char*)(w1 + (size_t)(c * 64 + wave * 16 + (lane & 15)) * 192 + s * 32 + g * 8));
-    const char* pb = yin + (tap * UPS + (half * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
+    const char* pb = yin + ((win ? 0 : tap * UPS) + (half * 32 + g * 8) / VE) * PL +
+                     ((win ? tap * d : 0) + (lane & 15)) * 16;
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
-      const Frag<T> bf = load_planes<T>(pb + p * 256, PLANE);
+      const Frag<T> bf = load_planes<T>(pb + p * 256, PL);
 #pragma unroll
       for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], af[c], bf);
     }
