@@ -58,3 +58,42 @@ def test_two_rank_gather_equals_single_run(tmp_path):
                          tables_from_golden("linear_3_0.0001_0.05"), noisy_speech(2, N, seed=1234),
                          "condition_in", seed=7)
     assert np.array_equal(np.load(out_path), full)
+
+
+def _spec_worker(rank, world, port, out_path):
+    """WaveGrad SDDM_spectrogram sampling of this rank's rows (row_offset = rank) + all_gather."""
+    sys.path.insert(0, os.path.dirname(HERE))
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "speech-denoising-diffusion-model-2_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import sampler, wavegrad as wg
+    from _helpers import tables_from_golden, wavegrad_params
+    P = wavegrad_params()
+    spec = np.random.default_rng(3).uniform(0, 1, (world, 128, 3)).astype(np.float32)[rank:rank + 1]
+    x = sampler.infer_spectrogram(lambda s, xx, nl: wg.forward(P, s, xx[:, 0], nl)[:, None],
+                                  tables_from_golden("linear_3_0.0001_0.05"), spec, wg.HOP, seed=7, row_offset=rank)
+    gathered = [torch.empty(1, 1, x.shape[-1]) for _ in range(world)]
+    dist.all_gather(gathered, torch.from_numpy(np.ascontiguousarray(x)))
+    if rank == 0:
+        np.save(out_path, torch.cat(gathered).numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_spectrogram_gather_equals_single_run(tmp_path):
+    """The same sharding contract for SDDM_spectrogram (WaveGrad): rows keyed by global index."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    out_path = str(tmp_path / "gathered_wg.npy")
+    mp.spawn(_spec_worker, args=(2, port, out_path), nprocs=2, join=True)
+    from oracle import sampler, wavegrad as wg
+    from _helpers import tables_from_golden, wavegrad_params
+    P = wavegrad_params()
+    spec = np.random.default_rng(3).uniform(0, 1, (2, 128, 3)).astype(np.float32)
+    full = sampler.infer_spectrogram(lambda s, xx, nl: wg.forward(P, s, xx[:, 0], nl)[:, None],
+                                     tables_from_golden("linear_3_0.0001_0.05"), spec, wg.HOP, seed=7)
+    assert np.array_equal(np.load(out_path), full)
