@@ -196,12 +196,12 @@ constexpr int WGL_MC = 128, WGL_HALO = 8;
 
 // TW = waves along time: block = 2 x TW waves = 128 channels x 64 TW positions (TW = 4 halves the
 // per-position weight traffic from L2 on the long levels)
-template <typename T, int PRE, int KT, int TW, int CK = 32>
+template <typename T, int PRE, int KT, int TW>
 __global__ __launch_bounds__(128 * TW) void wg_conv_lds_kernel(WGConvArgs a) {
 #pragma clang fp contract(off)
   constexpr int NT = 128 * TW, WGL_MT = 64 * TW;
   constexpr int ES = (int)sizeof(T), UE = 16 / ES;         // elements per 16-byte unit
-  constexpr int UPR = CK / UE;                              // units per CK-channel row
+  constexpr int UPR = 32 / UE;                              // units per 32-channel row
   constexpr int RS = UPR * 16 + 16;                         // padded LDS row stride (bytes)
   constexpr int SROWS = WGL_MT + 2 * WGL_HALO;
   constexpr int NBU = SROWS * UPR, NAU = KT * WGL_MC * UPR;
@@ -282,23 +282,20 @@ __global__ __launch_bounds__(128 * TW) void wg_conv_lds_kernel(WGConvArgs a) {
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc[i][p] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int wc = (wave & 1) * 64, wt = (wave >> 1) * 64;
-  const int ncs = Cin / CK;
+  const int ncs = Cin / 32;
   gload(0);
   for (int cc = 0; cc < ncs; ++cc) {
     __syncthreads();
     lstore();
     __syncthreads();
-    if (cc + 1 < ncs) gload((cc + 1) * CK);
+    if (cc + 1 < ncs) gload((cc + 1) * 32);
 #pragma unroll
-    for (int k = 0; k < KT; ++k)
-#pragma unroll
-    for (int h = 0; h < CK / 32; ++h) {
+    for (int k = 0; k < KT; ++k) {
       Frag<T> af[4], bf[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = load_frag<T>(wl + (k * WGL_MC + wc + i * 16 + l16) * RS + (h * 32 + g * 8) * ES);
+      for (int i = 0; i < 4; ++i) af[i] = load_frag<T>(wl + (k * WGL_MC + wc + i * 16 + l16) * RS + g * 8 * ES);
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
-        bf[p] = load_frag<T>(slab + (wt + p * 16 + l16 + k * a.dil) * RS + (h * 32 + g * 8) * ES);
+      for (int p = 0; p < 4; ++p) bf[p] = load_frag<T>(slab + (wt + p * 16 + l16 + k * a.dil) * RS + g * 8 * ES);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -346,11 +343,6 @@ bool wg_conv_uses_lds(const WGConvArgs& a) {
 template <typename T, int PRE, int TW>
 static void wg_conv_lds_dispatch(const WGConvArgs& a, hipStream_t s) {
   const dim3 grid((a.Tc + 64 * TW - 1) / (64 * TW), a.Cout / WGL_MC, a.B);
-  static const int ck_env = std::getenv("SDDM_WG_CK") ? std::atoi(std::getenv("SDDM_WG_CK")) : 32;
-  if (ck_env == 64 && a.Cin % 64 == 0 && a.K == 3) {       // 64-channel chunks: half the barriers
-    hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3, TW, 64>), grid, dim3(128 * TW), 0, s, a);
-    return;
-  }
   if (a.K == 1) hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE == 2 ? 0 : PRE, 1, TW>), grid, dim3(128 * TW), 0, s, a);
   else hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3, TW>), grid, dim3(128 * TW), 0, s, a);
 }
