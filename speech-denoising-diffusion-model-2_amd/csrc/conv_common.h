@@ -92,6 +92,35 @@ namespace sddm {
 // writes per-channel scale / shift = gamma*rstd, beta - mean*gamma*rstd into LDS.
 // Groups never straddle the A|B concat boundary (checked on the host).
 // ---------------------------------------------------------------------------------------------
+// Sum over the 16 lanes of a DPP row (lanes 16r .. 16r+15): four VALU adds with DPP operands
+// (xor 1, xor 2, mirror within 8, mirror within 16), every lane of the row ends with the sum.
+// __shfl_xor goes through the LDS crossbar (ds_bpermute) and a dependent chain of them costs a
+// full LDS round trip per step.
+template <int CTRL> __device__ __forceinline__ float dpp_f32(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float row_sum16(float x) {
+  x += dpp_f32<0xB1>(x);    // quad_perm [1,0,3,2]
+  x += dpp_f32<0x4E>(x);    // quad_perm [2,3,0,1]
+  x += dpp_f32<0x141>(x);   // row_half_mirror
+  x += dpp_f32<0x140>(x);   // row_mirror
+  return x;
+}
+
+// Sum over an aligned group of tpg lanes (a power of two; tpg is block-uniform): DPP steps
+// within 16 lanes, LDS-crossbar shuffles beyond
+__device__ __forceinline__ float group_sum(float x, int tpg) {
+  if (tpg > 1) x += dpp_f32<0xB1>(x);
+  if (tpg > 2) x += dpp_f32<0x4E>(x);
+  if (tpg > 4) x += dpp_f32<0x141>(x);
+  if (tpg > 8) x += dpp_f32<0x140>(x);
+  for (int o = 16; o < tpg; o <<= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+// largest power of two <= n (n >= 1)
+__device__ __forceinline__ int pow2_floor(int n) { return 1 << (31 - __builtin_clz(n)); }
+
 struct GNFuse {
   const float* statsA; int tilesA, ntileA;
   const float* statsB; int tilesB, ntileB;
@@ -101,7 +130,7 @@ struct GNFuse {
 
 __device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
   const int C = CA + CB, cpg = C / f.G;
-  const int tpg = blockDim.x / f.G;               // threads per group (power of two, <= 64)
+  const int tpg = pow2_floor(blockDim.x / f.G);   // threads per group (power of two, <= 64)
   const int g = threadIdx.x / tpg, sub = threadIdx.x - g * tpg;
   if (g >= f.G) return;
   const int c0 = g * cpg;
@@ -169,20 +198,24 @@ struct GNLoad {
   int items, tpg, sub, grp, ntile;
   bool fast;
 
-  __device__ __forceinline__ void issue(const GNFuse& f, int b, int CA, int CB) {
-    const int C = CA + CB, cpg = C / f.G;
-    tpg = blockDim.x / f.G;
+  // `on` = false (a conv without GroupNorm) still issues the same loads, all from `safe` (any
+  // readable address): the kernels call issue() unconditionally, because a load inside a branch
+  // makes the compiler wait for it at the branch join, serialising this round trip in front of
+  // every other load of the prologue.
+  __device__ __forceinline__ void issue(const GNFuse& f, int b, int CA, int CB, bool on, const float* safe) {
+    const int G = f.G > 0 ? f.G : 32;
+    const int C = CA + CB, cpg = C / G;
+    tpg = pow2_floor(blockDim.x / G);                 // xor butterflies: a power of two (6-wave blocks)
     grp = threadIdx.x / tpg;
     sub = threadIdx.x - grp * tpg;
-    const int c0 = grp * cpg;
+    const int c0 = min(grp, G - 1) * cpg;             // threads past the last group load group G-1's
     const bool fromA = c0 < CA;
-    const float* st = fromA ? f.statsA : f.statsB;
-    const int tiles = fromA ? f.tilesA : f.tilesB;
+    const int tiles = max(fromA ? f.tilesA : f.tilesB, 1);
     ntile = fromA ? f.ntileA : f.ntileB;
     const int Cs = fromA ? CA : CB;
     const int cs0 = fromA ? c0 : c0 - CA;
     items = cpg * tiles;
-    const float* base = st + (size_t)b * tiles * Cs * 2;
+    const float* base = on ? (fromA ? f.statsA : f.statsB) + (size_t)b * tiles * Cs * 2 : safe;
     const float rt = 1.0f / (float)tiles;
     // GK loads per thread, unconditional at clamped indices (a conditional load makes the
     // compiler drain the memory counter at the branch join); finish() ignores the items past the
@@ -193,12 +226,12 @@ struct GNLoad {
     for (int k = 0; k < GK; ++k) {
       const int i = min(sub + k * tpg, items - 1);
       const int c = fdivi(i, rt), t = i - c * tiles;
-      const int off = (t * Cs + cs0 + c) * 2;         // 32-bit offsets: no 64-bit address math
+      const int off = on ? (t * Cs + cs0 + c) * 2 : 0;   // 32-bit offsets: no 64-bit address math
       v[k] = *(const float2*)(base + off);
     }
-    const int cg = c0 + min(sub, cpg - 1);            // clamped: unconditional loads
-    gm = f.gamma[cg];
-    bt = f.beta[cg];
+    const int cg = on ? c0 + min(sub, cpg - 1) : 0;   // clamped: unconditional loads
+    gm = (on ? f.gamma : safe)[cg];
+    bt = (on ? f.beta : safe)[cg];
   }
 
   __device__ __forceinline__ void finish(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
@@ -215,7 +248,7 @@ struct GNLoad {
 #pragma unroll
     for (int k = 0; k < GK; ++k)
       if (sub + k * tpg < items) s += v[k].x;
-    for (int o = 1; o < tpg; o <<= 1) s += __shfl_xor(s, o);
+    s = group_sum(s, tpg);
     const float n_tot = (float)items * (float)ntile;
     const float r_tot = 1.0f / n_tot, r_tile = 1.0f / (float)ntile, fn = (float)ntile;
     const float mean = s * r_tot;
@@ -227,7 +260,7 @@ struct GNLoad {
         m2 += v[k].y + fn * d * d;
       }
     }
-    for (int o = 1; o < tpg; o <<= 1) m2 += __shfl_xor(m2, o);
+    m2 = group_sum(m2, tpg);
     const float rstd = 1.0f / sqrtf(m2 * r_tot + f.eps);
     if (sub < cpg) {
       const float scale = gm * rstd;
@@ -277,6 +310,11 @@ __device__ __forceinline__ void tile_channel_stats(const float* tile, int ld, in
 }  // namespace sddm
 
 namespace sddm {
+
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits for every outstanding
+// global load AND store of the wave (vmcnt(0)); in an epilogue that is the full write latency of
+// the stores just issued, on the critical path of the block, for nothing.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 

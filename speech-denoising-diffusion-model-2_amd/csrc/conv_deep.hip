@@ -111,7 +111,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   // ---------------- 1. issue every load of the block ----------------
   GNLoad gl;
   const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-  if (gn) gl.issue(gf, b, a.CA, a.CB);
+  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
 
   // staging units: [0, n3) halo planes (8 lanes = 8 consecutive halo pixels of one plane),
   // [n3, n3 + nres) raw res_conv input at the output pixels, then the identity-residual tile
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 
   // ---------------- 2. GroupNorm finalize, GN + SiLU into the LDS image ----------------
   if (gn && !(a.dbg & 1)) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
-  __syncthreads();                                       // scale / shift visible
+  lds_sync();                                            // scale / shift visible (loads stay in flight)
   SDDM_STAMP(a, 2);
 #pragma unroll
   for (int k = 0; k < MAXU; ++k)
@@ -233,15 +233,18 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) commit(reg[k], pk[k]);
   }
-  __syncthreads();
+  lds_sync();
   SDDM_STAMP(a, 3);
   // bias + noise embedding of this thread's 4 epilogue channels: in flight during the K loop
   const int ec4 = (tid & 7) * 4;
   float bb[4];
   {
-    const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : nullptr;
+    const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bb[i] = a.bias[n0 + ec4 + i] + (trow ? trow[n0 + ec4 + i] : 0.f);
+    for (int i = 0; i < 4; ++i) {                        // unconditional loads (no wait at a join)
+      const float bv = a.bias[n0 + ec4 + i], tv = trow[n0 + ec4 + i];
+      bb[i] = bv + (a.temb ? tv : 0.f);
+    }
   }
 
   // ---------------- 3. this wave's K steps ----------------
@@ -291,7 +294,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   SDDM_STAMP(a, 4);
 
   // ---------------- 4. reduce the partial tiles: red[slot][MT][NBP] ----------------
-  __syncthreads();                                       // every wave is done with the image
+  lds_sync();                                       // every wave is done with the image
   float* red = (float*)smem;
   auto put = [&](int slot) {
 #pragma unroll
@@ -303,7 +306,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   };
   if (SLOTS < NW) {                                      // waves 4..7 into slots, waves 0..3 add theirs
     if (wv >= SLOTS) put(wv - SLOTS);
-    __syncthreads();
+    lds_sync();
     if (wv < SLOTS) {
 #pragma unroll
       for (int fp = 0; fp < FP; ++fp) {
@@ -316,13 +319,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   } else {
     put(wv);
   }
-  __syncthreads();
+  lds_sync();
 
   constexpr int PPI = NT / 8;                            // pixels per epilogue pass
   constexpr int EIT = (MT + PPI - 1) / PPI;
-  float sn = 0.f, sk[4], s1[4], s2[4];
+  float sn = 0.f, s1[4], s2[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) { sk[i] = 0.f; s1[i] = 0.f; s2[i] = 0.f; }
+  for (int i = 0; i < 4; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
   T* out = (T*)a.out + (size_t)b * img_out * a.Cout + n0 + ec4;
 #pragma unroll
   for (int it = 0; it < EIT; ++it) {
@@ -332,83 +335,52 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
       f32x4 s = *(const f32x4*)(red + p * NBP + ec4);
 #pragma unroll
       for (int w = 1; w < SLOTS; ++w) s += *(const f32x4*)(red + (w * MT + p) * NBP + ec4);
-      float v[4];
+      float d[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) v[i] = s[i] + bb[i];
+      for (int i = 0; i < 4; ++i) d[i] = s[i];
       if (ident) {
         const T* rp = (const T*)(smem + lay.rres) + p * 32 + ec4;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) v[i] += to_f32<T>(rp[i]);
+        for (int i = 0; i < 4; ++i) d[i] += to_f32<T>(rp[i]);
       }
-      store4<T>(out + ((y0 + py) * a.Wo + (x0 + px)) * a.Cout, v[0], v[1], v[2], v[3]);
-      if (it == 0) {
+      store4<T>(out + ((y0 + py) * a.Wo + (x0 + px)) * a.Cout, d[0] + bb[0], d[1] + bb[1], d[2] + bb[2], d[3] + bb[3]);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) sk[i] = v[i];     // shift = first value (stable sums)
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float dlt = v[i] - sk[i];
-        s1[i] += dlt;
-        s2[i] += dlt * dlt;
+      for (int i = 0; i < 4; ++i) {                    // sums about the shift bb (the same for
+        s1[i] += d[i];                                 // every thread of a channel: they add)
+        s2[i] += d[i] * d[i];
       }
       sn += 1.f;
     }
   }
   SDDM_STAMP(a, 5);
   if (a.stats && !(a.dbg & 16)) {
-    // per-thread (n, mean, M2) -> lanes of one channel group (xor 8, 16, 32) -> waves via LDS;
-    // a full tile gives every epilogue thread the same count, so the merges need no division
-    constexpr int NWE = (MT / 8 < NW) ? MT / 8 : NW;    // waves holding epilogue pixels
-    const bool even = npv == MT;
-    float mn[4], m2[4], nn = sn;
+    // lanes l and l + 8 of a DPP row hold the same 4 channels (row_ror:8 add), then the 4 rows of
+    // every wave through LDS, summed by one thread per channel
+    const float tn = sn + dpp_f32<0x128>(sn);
+    float t1[4], t2[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float inv = sn > 0.f ? 1.0f / sn : 0.f;
-      mn[i] = sk[i] + s1[i] * inv;
-      m2[i] = fmaxf(s2[i] - s1[i] * s1[i] * inv, 0.f);
-    }
-    if (even) {
-#pragma unroll
-      for (int o = 8; o < 64; o <<= 1) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float mb = __shfl_xor(mn[i], o), qb = __shfl_xor(m2[i], o);
-          const float d = mb - mn[i];
-          m2[i] += qb + d * d * (nn * 0.5f);
-          mn[i] += 0.5f * d;
-        }
-        nn *= 2.f;
-      }
-    } else {
-      float nv[4] = {nn, nn, nn, nn};
-#pragma unroll
-      for (int o = 8; o < 64; o <<= 1)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const float nb = __shfl_xor(nv[i], o), mb = __shfl_xor(mn[i], o), qb = __shfl_xor(m2[i], o);
-          chan_merge(nv[i], mn[i], m2[i], nb, mb, qb);
-        }
-      nn = nv[0];
-    }
-    __syncthreads();                                   // red reads done
-    float* xs = red;                                   // [NWE waves][8 groups][4 ch][3]
-    if (wv < NWE && lane < 8)
+    for (int i = 0; i < 4; ++i) { t1[i] = s1[i] + dpp_f32<0x128>(s1[i]); t2[i] = s2[i] + dpp_f32<0x128>(s2[i]); }
+    lds_sync();                                        // red reads done
+    float* xs = red;                                   // [NW * 4 rows][NB channels][3]
+    if ((lane & 15) < 8)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float* e = xs + ((wave * 8 + lane) * 4 + i) * 3;
-        e[0] = nn; e[1] = mn[i]; e[2] = m2[i];
+        float* e = xs + ((wave * 4 + (lane >> 4)) * NB + ec4 + i) * 3;
+        e[0] = tn; e[1] = t1[i]; e[2] = t2[i];
       }
-    __syncthreads();
+    lds_sync();
     if (tid < NB) {
-      const int grp = tid >> 2, i = tid & 3;
-      float n = 0.f, mean = 0.f, q = 0.f;
-      for (int w = 0; w < NWE; ++w) {
-        const float* e = xs + ((w * 8 + grp) * 4 + i) * 3;
-        chan_merge(n, mean, q, e[0], e[1], e[2]);
+      float n = 0.f, u1 = 0.f, u2 = 0.f;
+#pragma unroll 4
+      for (int r = 0; r < NW * 4; ++r) {
+        const float* e = xs + (r * NB + tid) * 3;
+        n += e[0]; u1 += e[1]; u2 += e[2];
       }
+      const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : nullptr;
+      const float shift = a.bias[n0 + tid] + (trow ? trow[n0 + tid] : 0.f);
       float* dst = a.stats + (((size_t)b * a.n_tiles + tile) * a.Cout + n0 + tid) * 2;
-      dst[0] = mean * n;
-      dst[1] = q;
+      dst[0] = (shift + u1 / n) * n;
+      dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);
     }
   }
   SDDM_STAMP(a, 6);

@@ -71,7 +71,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   // ---------------- prologue: every independent load issued before anything waits ----------------
   GNLoad gl;
   const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-  if (gn) gl.issue(gf, b, a.CA, a.CB);
+  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
   // initial ring rows y0-1 .. y0+TR (raw), clamped addresses, zero rows outside the image later
   const T* srcAb = (const T*)a.srcA + (size_t)b * a.Hi * a.Wi * a.CA;
   const T* srcBb = a.CB ? (const T*)a.srcB + (size_t)b * a.Hi * a.Wi * a.CB : srcAb;
@@ -87,15 +87,23 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     const bool fa = c0 < a.CA;
     ini[k] = *(const f32x4*)((fa ? srcAb : srcBb) + ((size_t)sy * a.Wi + sx) * (fa ? a.CA : a.CB) + (fa ? c0 : c0 - a.CA));
   }
-  for (int u = tid; u < NBLK * WPLANES; u += NT) {        // co fastest: conflict-free LDS writes
+  // weight slabs straight into LDS (LDS-DMA: unit u lands at byte 16 u, co fastest, so every
+  // wave-instruction fills 1 KiB of consecutive LDS; no VGPRs, no wait until the first barrier)
+  // NBLK * WPLANES and NBLK * RPLANES are multiples of 64: whole waves, no tail
+  for (int u0 = wave * 64; u0 < NBLK * WPLANES; u0 += NT) {
+    const int u = u0 + lane;
     const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
     const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
-    *(f32x4*)(wl + pl * WPL + co * 16) =
-        *(const f32x4*)((const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16);
+    const char* src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(wl + u0 * 16), 16, 0, 0);
   }
-  for (int u = tid; u < NBLK * RPLANES; u += NT) {
+  for (int u0 = wave * 64; u0 < NBLK * RPLANES; u0 += NT) {
+    const int u = u0 + lane;
     const int co = u % NBLK, pl = u / NBLK;
-    *(f32x4*)(rw + pl * WPL + co * 16) = *(const f32x4*)((const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16);
+    const char* src = (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(rw + u0 * 16), 16, 0, 0);
   }
   for (int u = tid; u < R * UPP * 2; u += NT) {           // zero halo columns
     const int side = u & 1, pl = u >> 1;
@@ -103,6 +111,20 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   }
   if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + CIN);
   __syncthreads();                                         // gsc ready
+  // bias + noise embedding of this lane's epilogue channels: unconditional loads at clamped
+  // channels (a load under a condition is waited for at the branch join), issued before the
+  // initial ring commit so they are in flight during its GroupNorm + SiLU work
+  const int t_now = a.t_dev ? *a.t_dev : 0;
+  const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
+  float badd[FC][4];
+#pragma unroll
+  for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = n0 + fc * 16 + 4 * g + i, cc = min(co, a.Cout - 1);
+      const float bv = a.bias[cc], tv = trow[cc];
+      badd[fc][i] = (co < a.Cout) ? bv + (a.temb ? tv : 0.f) : 0.f;
+    }
   const int base = ((y0 - 1) % R + R) % R;                 // ring slot of row y0 - 1
 #pragma unroll
   for (int k = 0; k < IU; ++k) {
@@ -199,16 +221,6 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
     for (int i = 0; i < 4; ++i) { s1[fc][i] = 0.f; s2[fc][i] = 0.f; }
-  const int t_now = a.t_dev ? *a.t_dev : 0;
-  const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : nullptr;
-  float badd[FC][4];
-#pragma unroll
-  for (int fc = 0; fc < FC; ++fc)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = n0 + fc * 16 + 4 * g + i;
-      badd[fc][i] = (co < a.Cout) ? a.bias[co] + (trow ? trow[co] : 0.f) : 0.f;
-    }
   T* outb = (T*)a.out + (size_t)b * H * W * a.Cout;
   const char* abase = wl + g * UPL * WPL + (lane & 15) * 16;
   const char* rbase = rw + g * UPL * WPL + (lane & 15) * 16;
@@ -311,41 +323,31 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 
   SDDM_STAMP(a, 4);
   // ---- GroupNorm statistics of the strip: lanes -> waves -> block ----
+  // every lane of a channel sums about the same shift badd, so the sums add directly: the 16
+  // pixel lanes of a DPP row (VALU adds), then the waves through LDS
   if (a.stats) {
-    const float nl = (float)(FP * iters);
+    const float nl = (float)(FP * iters) * 16.f;
 #pragma unroll
     for (int fc = 0; fc < FC; ++fc)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        float n = nl;
-        float mean = badd[fc][i] + s1[fc][i] / nl;
-        float m2 = fmaxf(s2[fc][i] - s1[fc][i] * s1[fc][i] / nl, 0.f);
-#pragma unroll
-        for (int o = 1; o < 16; o <<= 1) {   // lanes with the same lane >> 4 hold the same channels
-          const float mo = __shfl_xor(mean, o), m2o = __shfl_xor(m2, o);
-          const float d = mo - mean;
-          m2 = m2 + m2o + d * d * (n * 0.5f);
-          mean = mean + 0.5f * d;
-          n *= 2.f;
-        }
+        const float t1 = row_sum16(s1[fc][i]), t2 = row_sum16(s2[fc][i]);
         if ((lane & 15) == 0) {
           float* rr = red + ((wave * NBLK) + fc * 16 + 4 * g + i) * 3;
-          rr[0] = n; rr[1] = mean; rr[2] = m2;
+          rr[0] = nl; rr[1] = t1; rr[2] = t2;
         }
       }
-    __syncthreads();
+    lds_sync();
     if (tid < NBLK && n0 + tid < a.Cout) {
-      float n = 0.f, mean = 0.f, m2 = 0.f;
+      float n = 0.f, u1 = 0.f, u2 = 0.f;
       for (int w = 0; w < NWV; ++w) {
         const float* rr = red + (w * NBLK + tid) * 3;
-        const float nb = rr[0], d = rr[1] - mean, nt = n + nb;
-        mean += d * nb / nt;
-        m2 += rr[2] + d * d * n * nb / nt;
-        n = nt;
+        n += rr[0]; u1 += rr[1]; u2 += rr[2];
       }
+      const float shift = a.bias[n0 + tid] + (a.temb ? trow[n0 + tid] : 0.f);
       float* dst = a.stats + (((size_t)b * a.n_tiles + strip) * a.Cout + n0 + tid) * 2;
-      dst[0] = mean * n;
-      dst[1] = m2;
+      dst[0] = (shift + u1 / n) * n;
+      dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);
     }
   }
   SDDM_STAMP(a, 6);

@@ -1,0 +1,425 @@
+// K-streamed implicit-GEMM 3x3 convolution for the middle and deep UNet levels (bf16 / f16):
+// Block / ResnetBlock convs, stride-2 Downsample and nearest-2x Upsample convs
+// (UNetModified2.py:93-142).  GEMM M = output pixels of one image tile, N = a block of NB output
+// channels, K = 9 taps x Cin, plus the 1x1 ResnetBlock.res_conv (UNetModified2.py:135) as extra
+// K chunks.
+//
+// Why this shape (measured on the whole-K kernel conv_deep.hip, which it replaces where it wins):
+// there a block of 32 output channels staged the GroupNorm + SiLU of its whole input halo, so the
+// transform of every input element ran Cout/32 times, and each wave pulled its weight fragments
+// as 16 rows x 64 B pieces.  Here
+//   * a block owns NB = 32..96 output channels, so an input element is transformed once per
+//     channel block (once per pixel for most layers), and up to 256 output pixels, so the weights
+//     a block streams are reused by that many pixels;
+//   * K runs in 32-channel chunks through a two-deep pipeline with one barrier per chunk: while
+//     the MFMAs of chunk k run, the raw input halo of chunk k+1 streams into registers and its
+//     weights into LDS by LDS-DMA (global_load_lds: no VGPRs, pre-packed chunk-major in
+//     ConvArgs::wgt_t so every DMA wave-instruction moves one contiguous 1 KiB run); after the
+//     MFMAs the same waves apply GroupNorm + SiLU to chunk k+1 and write its operand image;
+//   * 8-wave blocks keep two waves per SIMD, so one wave's VALU transform overlaps the other's
+//     MFMAs.
+// LDS operand images are plane-major (a plane = 8 channels, 16 B per pixel or output channel);
+// the pixel slot is XOR-swizzled by 2*plane so the staging writes (4 planes of 2 pixels per
+// 8-lane group) are conflict-free while any 16 consecutive slots of one plane still map to 16
+// distinct bank groups for the ds_read_b128 MFMA operand reads.  Stride-2 halos store even and
+// odd columns in separate halves so the taps of consecutive output pixels read consecutive slots.
+// Epilogue: bias + noise embedding + residual (identity, or the res_conv chunks), 4 channels per
+// lane stored as T, and GroupNorm tile statistics of the fp32 values (before the storage
+// rounding) as shifted sums reduced with DPP row adds, in the format every conv kernel consumes.
+#include "conv_common.h"
+#include "kernels.h"
+
+namespace sddm {
+
+// tile configurations: waves along pixels, waves along output channels, 16-pixel fragments per
+// wave, 16-channel fragments per wave, staging units per thread and chunk (stride 1 / stride 2)
+struct TileCfgX { int wpx, wco, fp, fc, maxu, maxu_s2; };
+static constexpr TileCfgX kTileCfgs[] = {
+    {4, 2, 4, 2, 4, 10},   //  0: 256 px x 64 co, 8 waves
+    {8, 1, 2, 2, 4, 10},   //  1: 256 px x 32 co, 8 waves
+    {4, 2, 2, 2, 3, 6},    //  2: 128 px x 64 co, 8 waves
+    {4, 2, 4, 3, 4, 10},   //  3: 256 px x 96 co, 8 waves
+    {4, 1, 2, 2, 5, 11},   //  4: 128 px x 32 co, 4 waves
+    {2, 2, 2, 2, 4, 8},    //  5:  64 px x 64 co, 4 waves
+    {2, 4, 2, 1, 2, 5},    //  6:  64 px x 64 co, 8 waves
+    {1, 4, 2, 1, 2, 5},    //  7:  32 px x 64 co, 4 waves
+    {1, 2, 2, 1, 2, 5},    //  8:  32 px x 32 co, 2 waves
+    {1, 1, 2, 1, 4, 10},   //  9:  32 px x 16 co, 1 wave
+    {4, 2, 2, 3, 3, 6},    // 10: 128 px x 96 co, 8 waves
+    {2, 1, 2, 2, 4, 10},   // 11:  64 px x 32 co, 2 waves
+};
+static constexpr int kNTileCfgs = (int)(sizeof(kTileCfgs) / sizeof(kTileCfgs[0]));
+
+struct TileGeo { int HR, HC, HE, HP, PLB, nu3, nur, ibb; };
+
+__host__ __device__ inline TileGeo tile_geo(bool s2, int TR, int TW, int MT, bool res) {
+  TileGeo g;
+  g.HR = s2 ? 2 * TR + 1 : TR + 2;
+  g.HC = s2 ? 2 * TW + 1 : TW + 2;
+  g.HE = (g.HC + 1) / 2;                                  // even halo columns (stride 2)
+  g.HP = g.HR * g.HC;
+  const int slots = g.HP > MT ? g.HP : MT;
+  g.PLB = (slots * 16 + 255) / 256 * 256;                 // plane bytes (the swizzle stays inside)
+  g.nu3 = g.HP * 4;                                       // 16-byte units of one 32-channel chunk
+  g.nur = res ? MT * 4 : 0;
+  g.ibb = 4 * g.PLB;
+  return g;
+}
+
+// LDS: two operand images, two weight chunks (576 B per output channel), GroupNorm scale / shift
+__host__ __device__ inline int tile_lds(const TileGeo& g, int NB, int Cin) {
+  return 2 * g.ibb + 2 * 576 * NB + 2 * Cin * 4;
+}
+
+__device__ __forceinline__ void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds, 16, 0, 0);
+}
+
+template <typename T, bool S2, int WPX, int WCO, int FP, int FC, int MAXU>
+__global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
+  constexpr int NWV = WPX * WCO, NT = 64 * NWV;
+  constexpr int MT = WPX * FP * 16, NB = WCO * FC * 16;
+  constexpr int WCH = 576 * NB;                            // LDS bytes of one 3x3 weight chunk
+  static_assert(sizeof(T) == 2, "conv_tile is the 16-bit path");
+  typedef T vec4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c16 = lane & 15, q = lane & 3;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wp = wv % WPX, wc = wv / WPX;
+  const int tile = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NB;
+  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
+  const int y0 = ty * a.TR, x0 = tx * a.TW;
+  const int npv = a.TR * a.TW;                             // valid pixels (< MT: image smaller than a tile)
+  const int Cin = a.CA + a.CB, nck = Cin / 32, ckA = a.CA / 32;
+  const int RC = a.RCA + a.RCB, rck = a.res_mode == 2 ? RC / 32 : 0, rckA = a.RCA / 32;
+  const int nk = nck + rck;
+  const bool gn = a.gamma != nullptr, ident = a.res_mode == 1;
+  const TileGeo geo = tile_geo(S2, a.TR, a.TW, MT, rck > 0);
+  const int HC = geo.HC, HE = geo.HE, PLB = geo.PLB;
+  char* IB = smem;                                         // [2][4 planes][PLB] operand images
+  char* WB = IB + 2 * geo.ibb;                             // [2][WCH]           weight chunks
+  float* gsc = (float*)(WB + 2 * WCH);                     // [2][Cin]           GroupNorm scale / shift
+  const float rHC = 1.0f / (float)HC, rTW = 1.0f / (float)a.TW;
+  const int img_in = a.Hi * a.Wi, img_out = a.Ho * a.Wo;
+  const T* srcA = (const T*)a.srcA + (size_t)b * img_in * a.CA;
+  const T* srcB = a.CB ? (const T*)a.srcB + (size_t)b * img_in * a.CB : srcA;
+  const T* rawA = rck ? (const T*)a.rawA + (size_t)b * img_out * a.RCA : srcA;
+  const T* rawB = (rck && a.RCB) ? (const T*)a.rawB + (size_t)b * img_out * a.RCB : rawA;
+  SDDM_STAMP(a, 0);
+
+  // ---------------- prologue: every independent load before anything waits ----------------
+  GNLoad gl;
+  const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
+  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
+  const int t_now = a.t_dev ? *a.t_dev : 0;
+  const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
+  const int cw0 = wc * FC * 16, pw0 = wp * FP * 16;
+  float bb[FC][4];
+#pragma unroll
+  for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {                          // unconditional loads (no wait at a join)
+      const int co = n0 + cw0 + fc * 16 + 4 * g + i;
+      const float bv = a.bias[co], tv = trow[co];
+      bb[fc][i] = bv + (a.temb ? tv : 0.f);
+    }
+  // this lane's output pixels (MFMA column c16 of each pixel fragment)
+  int ppy[FP], ppx[FP];
+  bool pok[FP];
+#pragma unroll
+  for (int fp = 0; fp < FP; ++fp) {
+    int p = pw0 + fp * 16 + c16;
+    pok[fp] = p < npv;
+    if (!pok[fp]) p = 0;
+    ppy[fp] = fdivi(p, rTW);
+    ppx[fp] = p - ppy[fp] * a.TW;
+  }
+  vec4 r1[FP][FC];                                         // identity residual (res_conv = Identity)
+  {
+    const T* rs = ident ? (const T*)a.res_src + (size_t)b * img_out * a.Cout : srcA;
+#pragma unroll
+    for (int fp = 0; fp < FP; ++fp) {
+      const int po = ident ? ((y0 + ppy[fp]) * a.Wo + (x0 + ppx[fp])) * a.Cout : 0;
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) r1[fp][fc] = *(const vec4*)(rs + po + (ident ? n0 + cw0 + fc * 16 + 4 * g : 0));
+    }
+  }
+  // staging geometry of this thread's 3x3 units (the same for every chunk): unit u = tid + j NT
+  // is plane q = u & 3 of halo slot u >> 2; source pixel (-1: zero padding), swizzled LDS offset
+  // (-1: past the halo)
+  int spx[MAXU], sof[MAXU];
+#pragma unroll
+  for (int j = 0; j < MAXU; ++j) {
+    const int u = tid + j * NT, s = u >> 2;
+    const int hy = fdivi(s, rHC), hx = s - hy * HC;
+    int iy, ix, slot;
+    bool ok;
+    if (S2) {
+      iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
+      ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+      slot = hy * HC + ((hx & 1) ? HE + (hx >> 1) : (hx >> 1));
+    } else {
+      iy = y0 - 1 + hy; ix = x0 - 1 + hx;
+      ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
+      if (a.upsample) { iy >>= 1; ix >>= 1; }
+      slot = s;
+    }
+    spx[j] = ok ? iy * a.Wi + ix : -1;
+    sof[j] = u < geo.nu3 ? q * PLB + ((slot ^ (q << 1)) << 4) : -1;
+  }
+
+  // raw chunk k -> registers (unconditional loads at clamped addresses)
+  f32x4 rr[MAXU];
+  auto load_raw = [&](int k) {
+    if (k < nck) {
+      const bool fa = k < ckA;
+      const T* base = (fa ? srcA + k * 32 : srcB + (k - ckA) * 32) + q * 8;
+      const int cs = fa ? a.CA : a.CB;
+#pragma unroll
+      for (int j = 0; j < MAXU; ++j) rr[j] = *(const f32x4*)(base + (spx[j] < 0 ? 0 : spx[j] * cs));
+    } else {                                               // res_conv chunk: raw input at the output pixels
+      const int r = k - nck;
+      const bool fa = r < rckA;
+      const T* base = (fa ? rawA + r * 32 : rawB + (r - rckA) * 32) + q * 8;
+      const int cs = fa ? a.RCA : a.RCB;
+#pragma unroll
+      for (int j = 0; j < MAXU; ++j) {
+        const int p = (tid + j * NT) >> 2;
+        const int py = fdivi(p, rTW), px = p - py * a.TW;
+        rr[j] = *(const f32x4*)(base + (p < npv ? ((y0 + py) * a.Wo + (x0 + px)) * cs : 0));
+      }
+    }
+  };
+  // weight chunk k -> WB[buf]: one contiguous run of NB units per (tap, plane)
+  auto issue_w = [&](int k, int buf) {
+    char* dst = WB + buf * WCH;
+    const bool res = k >= nck;
+    const int nw = (res ? 4 : 36) * NB;
+    const char* ws = res ? (const char*)a.res_wgt_t + (size_t)(k - nck) * 4 * a.Cout * 16
+                         : (const char*)a.wgt_t + (size_t)k * 36 * a.Cout * 16;
+    for (int u0 = wv * 64; u0 < nw; u0 += NT) {
+      const int u = u0 + lane, r = u / NB, co = u - r * NB;
+      glds16(ws + ((size_t)r * a.Cout + n0 + co) * 16, dst + u0 * 16);
+    }
+  };
+  // chunk k: registers -> IB[buf] with zero padding and GroupNorm + SiLU (3x3 chunks of a Block)
+  auto transform = [&](int k, int buf) {
+    char* ib = IB + buf * geo.ibb;
+    if (k < nck) {
+      float sc[8], sh[8];
+      if (gn) {
+        const int c = k * 32 + q * 8;
+#pragma unroll
+        for (int j = 0; j < 8; j += 4) {
+          const f32x4 s4 = *(const f32x4*)(gsc + c + j), h4 = *(const f32x4*)(gsc + Cin + c + j);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) { sc[j + i] = s4[i]; sh[j + i] = h4[i]; }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < MAXU; ++j) {
+        if (sof[j] < 0) continue;
+        f32x4 v = rr[j];
+        if (spx[j] < 0) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        else if (gn) v = transform_regs<T>(v, sc, sh);
+        *(f32x4*)(ib + sof[j]) = v;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < MAXU; ++j) {
+        const int u = tid + j * NT, p = u >> 2;
+        if (u >= geo.nur) continue;
+        f32x4 v = rr[j];
+        if (p >= npv) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        *(f32x4*)(ib + q * PLB + ((p ^ (q << 1)) << 4)) = v;
+      }
+    }
+  };
+
+  f32x4 acc[FP][FC];
+#pragma unroll
+  for (int i = 0; i < FP; ++i)
+#pragma unroll
+    for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // slot of tap (0, 0) for each pixel fragment of this lane
+  int sbase[FP];
+#pragma unroll
+  for (int fp = 0; fp < FP; ++fp) sbase[fp] = S2 ? 2 * ppy[fp] * HC + ppx[fp] : ppy[fp] * HC + ppx[fp];
+  const int gx = g << 1;
+  auto mma = [&](int k, int buf) {
+    const char* ib = IB + buf * geo.ibb + g * PLB;
+    const char* wb = WB + buf * WCH + (g * NB + cw0 + c16) * 16;
+    if (k < nck) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3, dx = tap - 3 * dy;
+        const int toff = S2 ? dy * HC + (dx == 0 ? 0 : (dx == 1 ? HE : 1)) : dy * HC + dx;
+        Frag<T> bf[FP];
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) bf[fp] = load_frag<T>(ib + (((sbase[fp] + toff) ^ gx) << 4));
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) {
+          const Frag<T> af = load_frag<T>(wb + (tap * 4 * NB + fc * 16) * 16);
+#pragma unroll
+          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
+        }
+      }
+    } else {
+      Frag<T> bf[FP];
+#pragma unroll
+      for (int fp = 0; fp < FP; ++fp) {
+        const int p = pok[fp] ? pw0 + fp * 16 + c16 : 0;
+        bf[fp] = load_frag<T>(ib + ((p ^ gx) << 4));
+      }
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) {
+        const Frag<T> af = load_frag<T>(wb + fc * 16 * 16);
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
+      }
+    }
+  };
+
+  load_raw(0);
+  issue_w(0, 0);
+  if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
+  SDDM_STAMP(a, 1);
+  __syncthreads();                                         // gsc visible
+  transform(0, 0);
+  __syncthreads();                                         // operand image 0, weights 0
+  SDDM_STAMP(a, 2);
+  for (int k = 0; k < nk; ++k) {
+    const int cur = k & 1, nxt = cur ^ 1;
+    if (k + 1 < nk) {
+      load_raw(k + 1);                                     // in flight during the MFMAs
+      issue_w(k + 1, nxt);                                 // WB[nxt] was read by chunk k - 1
+    }
+    mma(k, cur);
+    if (k + 1 < nk) transform(k + 1, nxt);                 // IB[nxt] was read by chunk k - 1
+    __syncthreads();
+  }
+  SDDM_STAMP(a, 4);
+
+  // ---------------- epilogue ----------------
+  T* out = (T*)a.out + (size_t)b * img_out * a.Cout;
+  float s1[FC][4], s2[FC][4], nl = 0.f;
+#pragma unroll
+  for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { s1[fc][i] = 0.f; s2[fc][i] = 0.f; }
+#pragma unroll
+  for (int fp = 0; fp < FP; ++fp) {
+    if (!pok[fp]) continue;
+    nl += 1.f;
+    const int po = ((y0 + ppy[fp]) * a.Wo + (x0 + ppx[fp])) * a.Cout;
+#pragma unroll
+    for (int fc = 0; fc < FC; ++fc) {
+      const int co = n0 + cw0 + fc * 16 + 4 * g;
+      float d[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) d[i] = acc[fp][fc][i] + (ident ? to_f32<T>(r1[fp][fc][i]) : 0.f);
+      store4<T>(out + po + co, d[0] + bb[fc][0], d[1] + bb[fc][1], d[2] + bb[fc][2], d[3] + bb[fc][3]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {                        // sums about the shift bb (stable)
+        s1[fc][i] += d[i];
+        s2[fc][i] += d[i] * d[i];
+      }
+    }
+  }
+  SDDM_STAMP(a, 5);
+  if (a.stats) {
+    // every lane of a channel uses the same shift, so the shifted sums add directly: the 16
+    // pixel lanes of a DPP row, then the WPX pixel waves through LDS
+    float* red = (float*)IB;                               // [WPX][NB][3] (operand images are dead)
+    const float nr = row_sum16(nl);
+#pragma unroll
+    for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float t1 = row_sum16(s1[fc][i]), t2 = row_sum16(s2[fc][i]);
+        if (c16 == 0) {
+          float* e = red + (wp * NB + cw0 + fc * 16 + 4 * g + i) * 3;
+          e[0] = nr; e[1] = t1; e[2] = t2;
+        }
+      }
+    lds_sync();
+    if (tid < NB) {
+      float n = 0.f, t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WPX; ++w) {
+        const float* e = red + (w * NB + tid) * 3;
+        n += e[0]; t1 += e[1]; t2 += e[2];
+      }
+      const int co = tid;                                   // bb of this channel: lane (co % 16) / 4 ...
+      const float shift = a.bias[n0 + co] + (a.temb ? trow[n0 + co] : 0.f);
+      const float mean = shift + t1 / n;
+      float* dst = a.stats + (((size_t)b * a.n_tiles + tile) * a.Cout + n0 + co) * 2;
+      dst[0] = mean * n;
+      dst[1] = fmaxf(t2 - t1 * t1 / n, 0.f);
+    }
+  }
+  SDDM_STAMP(a, 6);
+  SDDM_STAMP(a, 7);
+}
+
+template <int I>
+static size_t tile_lds_cfg(bool s2, const ConvArgs& a) {
+  constexpr TileCfgX c = kTileCfgs[I];
+  constexpr int MT = c.wpx * c.fp * 16, NB = c.wco * c.fc * 16;
+  const TileGeo g = tile_geo(s2, a.TR, a.TW, MT, a.res_mode == 2);
+  const int NT = 64 * c.wpx * c.wco, maxu = s2 ? c.maxu_s2 : c.maxu;
+  if (g.nu3 > maxu * NT || g.nur > maxu * NT) return (size_t)1 << 40;   // more staging units than registers
+  return (size_t)tile_lds(g, NB, a.CA + a.CB);
+}
+
+template <typename T, bool S2, int I>
+static hipError_t tile_go(const ConvArgs& a, int B, hipStream_t s) {
+  constexpr TileCfgX c = kTileCfgs[I];
+  constexpr int MT = c.wpx * c.fp * 16, NB = c.wco * c.fc * 16;
+  const size_t lds = tile_lds_cfg<I>(S2, a);
+  if (a.TR * a.TW > MT || a.Cout % NB || (a.CA + a.CB) % 32 || a.CA % 32 || (a.RCA + a.RCB) % 32 || a.RCA % 32 ||
+      lds > 160 * 1024 || !a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL((conv_tile_kernel<T, S2, c.wpx, c.wco, c.fp, c.fc, S2 ? c.maxu_s2 : c.maxu>),
+                     dim3(a.n_tiles, B, a.Cout / NB), dim3(64 * c.wpx * c.wco), lds, s, a);
+  return hipGetLastError();
+}
+
+template <typename T, bool S2>
+static hipError_t tile_dispatch(int cfg, const ConvArgs& a, int B, hipStream_t s) {
+  switch (cfg) {
+#define SDDM_TILE(I) \
+  case I: return tile_go<T, S2, I>(a, B, s);
+    SDDM_TILE(0) SDDM_TILE(1) SDDM_TILE(2) SDDM_TILE(3) SDDM_TILE(4) SDDM_TILE(5)
+    SDDM_TILE(6) SDDM_TILE(7) SDDM_TILE(8) SDDM_TILE(9) SDDM_TILE(10) SDDM_TILE(11)
+#undef SDDM_TILE
+    default: return hipErrorInvalidValue;
+  }
+}
+
+int conv_tile_ncfg() { return kNTileCfgs; }
+TileCfg conv_tile_cfg(int cfg) {
+  const TileCfgX& c = kTileCfgs[cfg];
+  return TileCfg{c.wpx, c.wco, c.fp, c.fc};
+}
+
+hipError_t launch_conv_tile(int dtype, int cfg, bool s2, const ConvArgs& a, int B, hipStream_t s) {
+  if (dtype == DT_BF16) return s2 ? tile_dispatch<bf16_t, true>(cfg, a, B, s) : tile_dispatch<bf16_t, false>(cfg, a, B, s);
+  if (dtype == DT_F16) return s2 ? tile_dispatch<f16_t, true>(cfg, a, B, s) : tile_dispatch<f16_t, false>(cfg, a, B, s);
+  return hipErrorInvalidValue;
+}
+
+size_t conv_tile_lds_bytes(int cfg, bool s2, const ConvArgs& a) {
+  switch (cfg) {
+#define SDDM_TILE(I) \
+  case I: return tile_lds_cfg<I>(s2, a);
+    SDDM_TILE(0) SDDM_TILE(1) SDDM_TILE(2) SDDM_TILE(3) SDDM_TILE(4) SDDM_TILE(5)
+    SDDM_TILE(6) SDDM_TILE(7) SDDM_TILE(8) SDDM_TILE(9) SDDM_TILE(10) SDDM_TILE(11)
+#undef SDDM_TILE
+    default: return (size_t)1 << 40;
+  }
+}
+
+}  // namespace sddm

@@ -74,7 +74,19 @@ struct ConvArgs {
   unsigned long long* stamps; // SDDM_STAMPS builds only: per-block phase timestamps [blocks][8]
   int dbg;                    // ablation flags for timing experiments (0 in production); conv_deep: 1 no GN
                               // finalize, 2 no GN+SiLU, 4 no staging loads, 8 no K loop, 16 no stats, 32 no weight loads
+  // conv_tile (16-bit dtypes): chunk-major weight images, one 16-byte unit = 8 input channels of
+  // one output channel: 3x3 [Cin/32][9][4][Cout][8], res_conv [RC/32][4][Cout][8]
+  const void* wgt_t;
+  const void* res_wgt_t;
 };
+
+// ---- K-streamed implicit-GEMM tile convolution (conv_tile.hip, bf16 / f16 only) ----
+// cfg: tile configuration index (kTileCfgs in conv_tile.hip); s2: stride-2 Downsample
+struct TileCfg { int wpx, wco, fp, fc; };   // waves along pixels / channels, 16-wide fragments per wave
+int conv_tile_ncfg();
+TileCfg conv_tile_cfg(int cfg);
+hipError_t launch_conv_tile(int dtype, int cfg, bool s2, const ConvArgs& a, int B, hipStream_t s);
+size_t conv_tile_lds_bytes(int cfg, bool s2, const ConvArgs& a);
 
 // ---- whole-K-resident tile convolution for the narrow levels (conv_deep.hip) ----
 // mt: output pixels per block (32 / 64 / 128); s2: stride-2 Downsample

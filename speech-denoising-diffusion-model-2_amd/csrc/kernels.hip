@@ -368,7 +368,7 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
   {
     const GNFuse gf{a.gst, a.gtiles, a.gntile, nullptr, 0, 0, a.gamma, a.beta, a.groups, a.eps};
     GNLoad gl;
-    gl.issue(gf, b, C, 0);
+    gl.issue(gf, b, C, 0, true, a.gamma);
     gl.finish(gf, b, C, 0, gs, gs + C);
   }
   __syncthreads();

@@ -289,6 +289,9 @@ struct sddm_ctx {
   // measured conv_deep tiles per layer name: (pixels per block, waves); valid for one lane batch /
   // dtype / num_samples (sddm_set_conv_tuning)
   std::map<std::string, std::pair<int, int>> deep_tune;
+  // per-layer kernel choice: 1 strip, 2 tile (a = configuration), 3 deep (a = pixels, b = waves)
+  struct KernTune { int kind, a, b; };
+  std::map<std::string, KernTune> kern_tune;
   int tune_B = -1, tune_dtype = -1, tune_N = -1;
   int hop_samples = 256;
 
@@ -338,6 +341,19 @@ static int upload_weights(sddm_ctx* c) {
     b.off = A.reserve(b.bytes.size());
     c->woff[name] = b.off;
     blobs.push_back(std::move(b));
+    if (dt != DT_F32) {  // conv_tile image [ci/32][9][4][co][8]: one 16-byte unit = 8 input channels
+      Blob bt;
+      bt.bytes.assign((size_t)co * ci * 9 * es, 0);
+      for (int o = 0; o < co; ++o)
+        for (int i = 0; i < ci; ++i)
+          for (int tap = 0; tap < 9; ++tap) {
+            const size_t dst = ((((size_t)(i / 32) * 9 + tap) * 4 + (i % 32) / 8) * co + o) * 8 + i % 8;
+            store_elem(bt.bytes.data(), dst, w.data[((size_t)o * ci + i) * 9 + tap], dt);
+          }
+      bt.off = A.reserve(bt.bytes.size());
+      c->woff[name + "_t"] = bt.off;
+      blobs.push_back(std::move(bt));
+    }
   };
   auto add_conv1 = [&](const std::string& name, const Param& w) {  // [co][ci] -> [co_pad64][ci]
     const int co = (int)w.shape[0], ci = (int)w.shape[1];
@@ -349,6 +365,17 @@ static int upload_weights(sddm_ctx* c) {
     b.off = A.reserve(b.bytes.size());
     c->woff[name] = b.off;
     blobs.push_back(std::move(b));
+    if (dt != DT_F32) {  // conv_tile image [ci/32][4][co][8]
+      Blob bt;
+      bt.bytes.assign((size_t)co * ci * es, 0);
+      for (int o = 0; o < co; ++o)
+        for (int i = 0; i < ci; ++i)
+          store_elem(bt.bytes.data(), (((size_t)(i / 32) * 4 + (i % 32) / 8) * co + o) * 8 + i % 8,
+                     w.data[(size_t)o * ci + i], dt);
+      bt.off = A.reserve(bt.bytes.size());
+      c->woff[name + "_t"] = bt.off;
+      blobs.push_back(std::move(bt));
+    }
   };
   const std::string pfx = "";
   std::vector<float> pw, pb;
@@ -433,6 +460,7 @@ struct ConvChoice {
   int strip = 0;      // 1: row-streaming kernel (conv_strip.hip), 0: whole-K tile kernel (conv_deep.hip)
   int nblk = 32, SR = 0, mpi = 128;
   int mt = 0, ckb = 0, nw = 4;                    // conv_deep: pixels per block, input chunks, waves
+  int tile = -1;                                  // conv_tile configuration (16-bit dtypes), -1: none
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
 };
 
@@ -482,8 +510,51 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
   return true;
 }
 
+// conv_tile configuration: the largest pixel x channel tile (most reuse of each transformed input
+// element and weight) among those whose grid still fills the chip; when no tile reaches 256
+// blocks, the one with the most blocks.  SDDM_TILE_CFG=<i> forces configuration i wherever it
+// fits; SDDM_NO_TILE=1 keeps every 16-bit layer on conv_deep (experiments).
+static bool choose_tile(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int want = -1) {
+  if (dt == DT_F32) return false;
+  static const int force = std::getenv("SDDM_TILE_CFG") ? std::atoi(std::getenv("SDDM_TILE_CFG")) : -1;
+  static const bool off = std::getenv("SDDM_NO_TILE") != nullptr;
+  if (off) return false;
+  const int fw = want >= 0 ? want : force;
+  struct Cand { int cfg, TR, TW, tiles_x, n_tiles, blocks, area; };
+  std::vector<Cand> cs;
+  for (int cfg = 0; cfg < conv_tile_ncfg(); ++cfg) {
+    const TileCfg t = conv_tile_cfg(cfg);
+    const int MT = t.wpx * t.fp * 16, NB = t.wco * t.fc * 16;
+    if (a.Cout % NB) continue;
+    const int TW = std::min(a.Wo, MT);
+    if (MT % TW || a.Wo % TW) continue;
+    const int TR = std::min(MT / TW, a.Ho);
+    if (a.Ho % TR) continue;
+    if (TR * TW < MT && (TR != a.Ho || TW != a.Wo)) continue;   // partial tiles: whole small images only
+    a.TR = TR; a.TW = TW; a.tiles_x = a.Wo / TW; a.n_tiles = a.tiles_x * (a.Ho / TR);
+    if (conv_tile_lds_bytes(cfg, s2, a) > 160 * 1024) continue;
+    cs.push_back({cfg, TR, TW, a.tiles_x, a.n_tiles, a.n_tiles * B * (a.Cout / NB), TR * TW * NB});
+  }
+  if (cs.empty()) return false;
+  const Cand* pick = nullptr;
+  for (const Cand& c : cs)
+    if (c.cfg == fw) pick = &c;
+  if (!pick) {
+    for (const Cand& c : cs) {
+      if (!pick) { pick = &c; continue; }
+      const bool cf = c.blocks >= 256, pf = pick->blocks >= 256;
+      if (cf != pf) { if (cf) pick = &c; continue; }
+      if (!cf) { if (c.blocks != pick->blocks) { if (c.blocks > pick->blocks) pick = &c; continue; } }
+      if (c.area > pick->area) pick = &c;
+    }
+  }
+  ch.strip = 0; ch.tile = pick->cfg;
+  ch.TR = pick->TR; ch.TW = pick->TW; ch.tiles_x = pick->tiles_x; ch.n_tiles = pick->n_tiles;
+  return true;
+}
+
 static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
-                        ConvChoice& ch, int want_mt = 0, int want_nw = 0) {
+                        ConvChoice& ch, int want_mt = 0, int want_nw = 0, int kind = 0, int ka = 0) {
   ConvArgs a{};
   a.CA = Cin; a.CB = 0; a.RCA = RC; a.RCB = 0; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.upsample = up ? 1 : 0;
@@ -491,7 +562,11 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
   // tuning knobs for experiments (unset = defaults): SDDM_STRIP_MPI=128|256, SDDM_STRIP_BLOCKS=target grid
   static const int env_mpi = std::getenv("SDDM_STRIP_MPI") ? std::atoi(std::getenv("SDDM_STRIP_MPI")) : 0;
   static const int env_blocks = std::getenv("SDDM_STRIP_BLOCKS") ? std::atoi(std::getenv("SDDM_STRIP_BLOCKS")) : 0;
-  if (!s2 && (Wo == 128 || Wo == 64) && std::getenv("SDDM_NO_STRIP") == nullptr) {
+  if (kind == 2) {
+    ConvChoice t = ch;
+    if (choose_tile(dt, B, a, s2, t, ka) && t.tile == ka) { ch = t; return true; }
+  }
+  if (!s2 && (Wo == 128 || Wo == 64) && std::getenv("SDDM_NO_STRIP") == nullptr && (kind == 0 || kind == 1)) {
     const int nbs[2] = {(Cout % 64 == 0) ? 64 : 32, 32};
     for (int mpi : {256, 128}) {
       if (env_mpi && mpi != env_mpi) continue;
@@ -516,6 +591,7 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
       }
     }
   }
+  if (want_mt == 0 && kind != 3 && choose_tile(dt, B, a, s2, ch)) return true;
   return choose_deep(dt, B, a, s2, ch, want_mt, want_nw);
 }
 
@@ -565,15 +641,24 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   std::vector<Step> prog;
   // measured per-layer deep tiles (sddm_set_conv_tuning) apply when they were measured for this
   // lane batch, dtype and length; otherwise the round-count heuristic of choose_deep decides
-  const bool tuned = c->tune_B == B && c->tune_dtype == dt && c->tune_N == N;
+  // kernel choices depend on the geometry and the lane capacity, never on the rows a lane holds:
+  // every lane, and every row partition of a batch (sharded runs), gets the same kernels, tiles
+  // and GroupNorm tilings, hence bit-identical rows
+  const int PB = std::max(1, c->lane_rows);
+  const bool tuned = c->tune_B == PB && c->tune_dtype == dt && c->tune_N == N;
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
-    int wm = 0, wn = 0;
+    int wm = 0, wn = 0, kind = 0, ka = 0;
     if (tuned) {
       auto it = c->deep_tune.find(name);
-      if (it != c->deep_tune.end()) { wm = it->second.first; wn = it->second.second; }
+      if (it != c->deep_tune.end()) { wm = it->second.first; wn = it->second.second; kind = 3; }
+      auto kt = c->kern_tune.find(name);
+      if (kt != c->kern_tune.end()) {
+        kind = kt->second.kind; ka = kt->second.a;
+        if (kind == 3) { wm = kt->second.a; wn = kt->second.b; }
+      }
     }
-    return choose_conv(dt, B, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn);
+    return choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka);
   };
   const int TRin = 512 / W;
   if (u.inner != 32 || 512 % W || F % TRin || (TRin + 1) * S + W + 2 > 1024)
@@ -694,6 +779,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           FAIL(SDDM_ERR_SHAPE, "GroupNorm(%d, %d) at %s: unsupported grouping", u.groups, Ct, gr.w.c_str());
       }
       a.wgt = WV(st.w + ".w"); a.bias = WF(st.w + ".b");
+      a.wgt_t = c->woff.count(st.w + ".w_t") ? WV(st.w + ".w_t") : nullptr;
       a.res_mode = st.res_mode;
       const int Cin = a.CA + a.CB;
       double bytes = (double)B * a.Hi * a.Wi * Cin * es + (double)B * a.Ho * a.Wo * a.Cout * es +
@@ -706,6 +792,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         const Tensor ra = TT(st.rawA), rb = TT(st.rawB);
         a.rawA = ra.p; a.rawB = rb.p; a.RCA = ra.C; a.RCB = rb.C;
         a.res_wgt = WV(st.rb + ".res.w");
+        a.res_wgt_t = c->woff.count(st.rb + ".res.w_t") ? WV(st.rb + ".res.w_t") : nullptr;
         if ((ra.C + rb.C) % 32) FAIL(SDDM_ERR_SHAPE, "%s.res_conv: channels must be multiples of 32", st.rb.c_str());
         bytes += (double)B * a.Ho * a.Wo * (ra.C + rb.C) * es + (double)a.Cout * (ra.C + rb.C) * es;
         flops += 2.0 * B * a.Ho * a.Wo * a.Cout * (double)(ra.C + rb.C);
@@ -737,9 +824,10 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                             x.t_dev = lp->rs.t_dev;
                           }
                           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
+                          if (ch.tile >= 0) return launch_conv_tile(dt, ch.tile, s2, x, B, s);
                           x.ck_batch = ch.ckb; x.deep_nw = ch.nw;
                           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
-                        }, st.w + (ch.strip ? "[strip]" : "")});
+                        }, st.w + (ch.strip ? "[strip]" : (ch.tile >= 0 ? "[tile" + std::to_string(ch.tile) + "]" : ""))});
       {  // flags: 1 no stats, 2 no GroupNorm transform, 4 no residual / embedding, 8 skip the K loop
         auto base = L.ops.back().run;
         ConvArgs a0 = a;
@@ -751,6 +839,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           if (fl & 4) x.res_mode = 0;
           x.dbg = fl;
           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
+          if (ch.tile >= 0) return launch_conv_tile(dt, ch.tile, s2, x, B, s);
           x.ck_batch = ch.ckb; x.deep_nw = ch.nw;
           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
         };
@@ -1342,10 +1431,26 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
   const std::string dts = j.string("dtype", "");
   const int dt = dts == "float32" ? DT_F32 : dts == "bfloat16" ? DT_BF16 : dts == "float16" ? DT_F16 : -1;
   c->deep_tune.clear();
-  for (const auto& kv : j.at("deep").obj) {
-    if (kv.second.kind != Json::ARR || kv.second.arr.size() != 2) FAIL(SDDM_ERR_INVALID_ARG, "deep.%s: [mt, nw]", kv.first.c_str());
-    c->deep_tune[kv.first] = {(int)kv.second.arr[0].num, (int)kv.second.arr[1].num};
-  }
+  c->kern_tune.clear();
+  if (j.has("deep"))
+    for (const auto& kv : j.at("deep").obj) {
+      if (kv.second.kind != Json::ARR || kv.second.arr.size() != 2) FAIL(SDDM_ERR_INVALID_ARG, "deep.%s: [mt, nw]", kv.first.c_str());
+      c->deep_tune[kv.first] = {(int)kv.second.arr[0].num, (int)kv.second.arr[1].num};
+    }
+  // "kernel": {"<layer>": "strip" | "tile:<cfg>" | "deep" | "deep:<mt>:<nw>"}
+  if (j.has("kernel"))
+    for (const auto& kv : j.at("kernel").obj) {
+      if (kv.second.kind != Json::STR) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: a string", kv.first.c_str());
+      const std::string& v = kv.second.str;
+      sddm_ctx::KernTune t{0, 0, 0};
+      if (v == "strip") t.kind = 1;
+      else if (v.rfind("tile:", 0) == 0) { t.kind = 2; t.a = std::atoi(v.c_str() + 5); }
+      else if (v == "deep") t.kind = 3;
+      else if (v.rfind("deep:", 0) == 0) { t.kind = 3; std::sscanf(v.c_str() + 5, "%d:%d", &t.a, &t.b); }
+      else FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: unknown choice '%s'", kv.first.c_str(), v.c_str());
+      if (t.kind == 2 && (t.a < 0 || t.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), t.a);
+      c->kern_tune[kv.first] = t;
+    }
   c->tune_B = (int)j.number("lane_batch", -1);
   c->tune_dtype = dt;
   c->tune_N = (int)j.number("num_samples", -1);

@@ -64,7 +64,7 @@ class SDDM(nn.Module):
         if self._ctx is None or self._ctx_key != key:
             ctx = sddm_hip.Context(self.library_config(), device.index or 0, self.compute_dtype)
             ctx.load_state_dict(sd)
-            if os.path.exists(_TUNING):           # measured conv tiles (tools/tune_deep.py)
+            if os.path.exists(_TUNING) and not os.environ.get("SDDM_NO_TUNING"):   # measured per-layer kernels
                 with open(_TUNING) as f:
                     ctx.set_conv_tuning(f.read())
             self._ctx, self._ctx_key = ctx, key

@@ -69,3 +69,45 @@ def test_diffwave_row_sharding_is_bit_identical(torch_cuda):
     a = m.infer(spec[:2].contiguous(), seed=5, row_offset=0)
     b = m.infer(spec[2:].contiguous(), seed=5, row_offset=2)
     assert torch.equal(full, torch.cat([a, b]))
+
+
+def _dw_rows(B, F, seed):
+    rng = np.random.default_rng(seed)
+    spec = rng.uniform(0, 1, (B, 513, F)).astype(np.float32)          # U[0,1]
+    audio = rng.standard_normal((B, 1, 256 * F)).astype(np.float32)
+    steps = rng.integers(1, 201, B).astype(np.float32)              # time_step conditioning, T=200
+    return spec, audio, steps
+
+
+@pytest.mark.parametrize("dtype,tol", [("float32", 1e-4), ("bfloat16", 3e-2)])
+def test_diffwave_config3_geometry(torch_cuda, dtype, tol):
+    """Config #3 geometry (config_diffwave.json: 63 frames x hop 256 = 16128 samples): 4 distinct
+    rows at 4 diffusion steps against the numpy oracle -- covers the dilation <= 64 shared-window
+    staging, the layer-major conditioner / z layouts and every partial tile of the layer kernel."""
+    from oracle import diffwave as odw
+    B, F = 4, 63
+    spec, audio, steps = _dw_rows(B, F, 31)
+    ref = odw.forward(diffwave_params(), spec, audio, steps)
+    eps = _net(dtype)(torch.from_numpy(spec).cuda(), torch.from_numpy(audio).cuda(),
+                      torch.from_numpy(steps).reshape(-1, 1, 1).cuda()).cpu().numpy()
+    for b in range(B):
+        err = rms(eps[b], ref[b])
+        print(f"{dtype} row {b} step {steps[b]:.0f}: rms {err:.3e} (ref rms {rms(ref[b], 0):.3f})")
+        assert err <= tol * max(1.0, rms(ref[b], 0))
+
+
+def test_diffwave_config3_bench_batch(torch_cuda):
+    """The benchmarked launch plan (B=64 x 63 frames, bf16) on 64 distinct rows; a spread of rows
+    is checked against the oracle (a lane / row-offset error would show on these)."""
+    from oracle import diffwave as odw
+    B, F = 64, 63
+    spec, audio, steps = _dw_rows(B, F, 32)
+    eps = _net("bfloat16")(torch.from_numpy(spec).cuda(), torch.from_numpy(audio).cuda(),
+                           torch.from_numpy(steps).reshape(-1, 1, 1).cuda()).cpu().numpy()
+    assert np.isfinite(eps).all()
+    rows = [0, 21, 42, 63]
+    ref = odw.forward(diffwave_params(), spec[rows], audio[rows], steps[rows])
+    for i, b in enumerate(rows):
+        err = rms(eps[b], ref[i])
+        print(f"bf16 B=64 row {b}: rms {err:.3e}")
+        assert err <= 3e-2 * max(1.0, rms(ref[i], 0))

@@ -59,31 +59,65 @@ def test_unet_forward_reduced_precision(torch_cuda, dtype, tol):
     assert err <= tol
 
 
-@pytest.mark.parametrize("dtype,tol,tuned", [("float32", 1e-4, False), ("bfloat16", 2.5e-2, False),
-                                            ("bfloat16", 2.5e-2, True)])
+_BENCH_ROWS = {}
+
+
+def bench_rows(N=16448, B=16):
+    """16 distinct rows of the bench shape: VoiceBank-shaped conditions, x_t drawn at 16 different
+    noise levels of the headline schedule (linear 1e-6..1e-3, T=1000), and the numpy oracle's
+    fp32 forward of every row (pinned to the reference goldens by tests/test_oracle.py)."""
+    if (N, B) not in _BENCH_ROWS:
+        from oracle import schedule as osched
+        from oracle import unet as ounet
+        from sddm_hip.synth import noisy_speech
+        from _helpers import unet_arch
+        tab = osched.make_tables("linear", 1000, 1e-6, 1e-3)
+        ts = np.linspace(1000, 1, B).round().astype(int)
+        nl = tab["sqrt_alpha_bar"][ts].astype(np.float32)
+        cond = noisy_speech(B, N, seed=21)
+        z = np.random.default_rng(22).standard_normal((B, 1, N)).astype(np.float32)
+        x_t = (nl[:, None, None] * cond + np.sqrt(1 - nl[:, None, None] ** 2) * z).astype(np.float32)
+        ref = ounet.forward(unet_params(N), unet_arch(N), cond, x_t, nl)
+        _BENCH_ROWS[(N, B)] = (cond, x_t, nl, ref)
+    return _BENCH_ROWS[(N, B)]
+
+
+# per-layer kernel table exercising every kernel family on the bench geometry (tile configurations
+# of 1, 2, 4, 6 and 8 waves, stride 2, upsample, virtual concat, res_conv chunks, conv_deep tiles)
+_TUNING = {"downs.4": "tile:2", "downs.5.block1": "tile:10", "downs.5.block2": "tile:6", "downs.6": "tile:4",
+           "downs.7.block1": "tile:8", "downs.8": "tile:7", "downs.9.block2": "deep:32:8", "downs.10": "tile:9",
+           "mid.0.block1": "tile:8", "mid.0.block2": "deep", "ups.0.block1": "tile:9", "ups.4": "tile:6",
+           "ups.5.block1": "tile:11", "ups.7": "tile:3", "ups.8.block1": "tile:1", "ups.8.block2": "tile:0",
+           "ups.11.block1": "tile:1", "ups.12.block1": "strip"}
+
+
+@pytest.mark.parametrize("dtype,tol,tuned", [("float32", 1e-4, None), ("bfloat16", 2.5e-2, None),
+                                            ("bfloat16", 2.5e-2, "table"), ("bfloat16", 2.5e-2, "repo"),
+                                            ("float16", 5e-3, None)])
 def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
-    """B=16 x N=16448 (the bench shape): the kernel/tile configurations picked for a full batch
-    (not the B=1 ones) -- and per-layer tiles set through sddm_set_conv_tuning -- reproduce the
-    reference on every row; rows use mixed noise levels."""
+    """B=16 x N=16448 (the bench shape), 16 distinct rows at 16 noise levels: the kernels and tiles
+    picked for a full lane (and per-layer kernels set through sddm_set_conv_tuning: a table
+    covering every kernel family, and the repository's measured table) reproduce the oracle on
+    every row, so no row-offset / lane / per-row embedding error can hide behind identical rows."""
+    import os
     N, B = 16448, 16
-    fw = golden("unet_forward.npz")
+    cond, x_t, nl, ref = bench_rows(N, B)
     dev = torch_cuda.device("cuda", 0)
-    cond = np.repeat(fw[f"fw/{N}/cond"], B, axis=0)
-    x_t = np.repeat(fw[f"fw/{N}/x_t"], B, axis=0)
-    nl = np.repeat(fw[f"fw/{N}/noise_level"], B, axis=0)
     ctx = make_ctx(N, dtype)
-    if tuned:     # sddm_set_conv_tuning: per-layer conv_deep tiles other than the heuristic's
-        ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N,
-                             "deep": {"downs.6": [64, 4], "downs.8": [32, 8], "mid.0.block1": [32, 8],
-                                      "ups.5.block1": [64, 4], "ups.7": [128, 4]}})
+    if tuned == "table":
+        ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N, "kernel": _TUNING})
+    elif tuned == "repo":
+        path = os.path.join(os.path.dirname(sddm_hip.__file__), "..", "configs", "conv_tuning.json")
+        if not os.path.exists(path):
+            pytest.skip("no measured per-layer table in the repository")
+        ctx.set_conv_tuning(open(path).read())
     eps = torch_cuda.full((B, 1, N), float("nan"), device=dev)
     ctx.network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
                         torch_cuda.from_numpy(nl).to(dev), eps)
     torch_cuda.cuda.synchronize()
     eps = eps.cpu().numpy()
-    ref = fw[f"fw/{N}/eps"][0]
-    errs = [rms(eps[b], ref) for b in range(B)]
-    print(f"{dtype} B={B} forward: worst row rms {max(errs):.3e}")
+    errs = [rms(eps[b], ref[b]) for b in range(B)]
+    print(f"{dtype} {tuned} B={B} forward: row rms min {min(errs):.3e} max {max(errs):.3e} (ref rms {rms(ref, 0):.3f})")
     assert np.isfinite(eps).all()
     assert max(errs) <= tol
 
@@ -188,3 +222,46 @@ def test_unet_forward_config5_geometry(torch_cuda, dtype, tol):
     err = rms(got, ref)
     print(f"{dtype} forward N={N}: rms err {err:.3e}")
     assert err <= tol
+
+
+def test_multilane_graph_replay_equals_row_blocks(torch_cuda, monkeypatch):
+    """B=40 = three lanes of 16 rows (graph-replayed concurrently on three streams, each lane with
+    its own step counter and row offset) equals separate calls on the row blocks, bit for bit;
+    the non-graph path gives the same bits; 4-row lanes (10 lanes on 4 streams) equal their own
+    row blocks and stay close to the 16-row-lane result."""
+    from sddm_hip.synth import noisy_speech
+    N, B, sched = 2112, 40, ("linear", 6, 1e-6, 1e-3)
+    cond = noisy_speech(B, N, seed=77)
+    ctx = make_ctx(N, "bfloat16", sched)
+    full = _sample(torch_cuda, ctx, cond)
+    blocks = np.concatenate([_sample(torch_cuda, ctx, cond[r:r + 16], row_offset=r) for r in (0, 16, 32)])
+    assert np.isfinite(full).all()
+    assert np.array_equal(full, blocks)
+    monkeypatch.setenv("SDDM_NO_GRAPH", "1")
+    assert np.array_equal(_sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond), full)
+    monkeypatch.delenv("SDDM_NO_GRAPH")
+    monkeypatch.setenv("SDDM_LANE_ROWS", "4")
+    ctx4 = make_ctx(N, "bfloat16", sched)
+    full4 = _sample(torch_cuda, ctx4, cond)
+    blocks4 = np.concatenate([_sample(torch_cuda, ctx4, cond[r:r + 8], row_offset=r) for r in range(0, B, 8)])
+    assert np.array_equal(full4, blocks4)
+    err = rms(full4, full)
+    print(f"4-row lanes vs 16-row lanes: rms {err:.3e}")
+    assert err <= 1e-2
+
+
+def test_headline_bf16_vs_fp32_1000_steps(torch_cuda):
+    """The benchmarked workload (config #2: T=1000, B=16 x 16448, linear 1e-6..1e-3, condition_in)
+    sampled in bf16 and in fp32 on the HIP path from the same seed: the RMS difference of the
+    denoised outputs is the bf16 drift DESIGN.md §4 quotes (fp32 itself is pinned to the reference
+    at <= 1.2e-7 RMS by the sampling-loop tests)."""
+    from sddm_hip.synth import noisy_speech
+    N, B, sched = 16448, 16, ("linear", 1000, 1e-6, 1e-3)
+    cond = noisy_speech(B, N, seed=1234)
+    out32 = _sample(torch_cuda, make_ctx(N, "float32", sched), cond)
+    out16 = _sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond)
+    assert np.isfinite(out16).all() and np.isfinite(out32).all()
+    err = rms(out16, out32)
+    rows = [rms(out16[b], out32[b]) for b in range(B)]
+    print(f"T=1000 B=16 bf16 vs fp32: rms {err:.3e}, worst row {max(rows):.3e}, signal rms {rms(out32, 0):.3f}")
+    assert err <= 5e-3

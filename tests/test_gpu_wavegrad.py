@@ -93,3 +93,22 @@ def test_wavegrad_single_clip_squeezes_like_reference(torch_cuda):
     assert tuple(out.shape) == (900,)
     ref = wg.forward(wavegrad_params(), spec, audio, nl)[0]
     assert rms(out.cpu().numpy(), ref) <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref ** 2))))
+
+
+def test_wavegrad_bf16_bench_batch(torch_cuda):
+    """Config #4 per-GPU shape (B=64 x 54 frames x hop 300, bf16, the LDS-tiled conv plan) on 64
+    distinct rows; a spread of rows is checked against the numpy oracle."""
+    from oracle import wavegrad as wg
+    B, F = 64, 54
+    rng = np.random.default_rng(41)
+    spec = rng.uniform(0, 1, (B, 128, F)).astype(np.float32)
+    audio = rng.standard_normal((B, 300 * F)).astype(np.float32)
+    nl = rng.uniform(0.05, 0.99, B).astype(np.float32)
+    eps = _net("bfloat16")(*(torch.from_numpy(x).cuda() for x in (spec, audio, nl))).cpu().numpy()
+    assert np.isfinite(eps).all()
+    rows = [0, 19, 44, 63]
+    ref = wg.forward(wavegrad_params(), spec[rows], audio[rows], nl[rows])
+    for i, b in enumerate(rows):
+        err = rms(eps[b], ref[i])
+        print(f"bf16 B=64 row {b}: rms {err:.3e} (ref rms {rms(ref[i], 0):.3f})")
+        assert err <= 3e-2 * max(1.0, rms(ref[i], 0))

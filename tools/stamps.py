@@ -61,8 +61,8 @@ def main():
         span = (t7.max() - t0.min()) * 10e-3
         dur = (t7 - t0) * 10e-3
         start = (t0 - t0.min()) * 10e-3
-        ph = [f"{k}->{k + 1}: {np.mean(st[:, k + 1] - st[:, k]):8.0f}" for k in range(1, 6)
-              if st[:, k].any() and st[:, k + 1].any()]
+        nz = [k for k in range(1, 7) if st[:, k].any()]
+        ph = [f"{k0}->{k1}: {np.mean(st[:, k1] - st[:, k0]):8.0f}" for k0, k1 in zip(nz[:-1], nz[1:])]
         cyc = st[:, 6] - st[:, 1] if st[:, 1].any() else st[:, 6] - st[:, 3]
         print(f"{op}: {n.value} blocks, span {span:.1f} us, block dur mean {dur.mean():.2f} max {dur.max():.2f} us, "
               f"start spread max {start.max():.2f} us (p50 {np.median(start):.2f})")
