@@ -1,8 +1,9 @@
 """ORACLE (test infrastructure only) — log-magnitude (mel) spectrogram in numpy.
 
-Restates prepare_spectrogram.py:20-55 of the reference, i.e. torchaudio.transforms.Spectrogram /
-MelSpectrogram(power=1, normalized=True, hamming window, center=True, reflect padding) followed
-by clamp((log10(S) - 1 + 5) / 5, 0, 1).  torchaudio (unpinned by the reference, absent here) is
+Restates prepare_spectrogram.py:20-55 of the reference, i.e. torchaudio.transforms.Spectrogram
+(Hamming window, prepare_spectrogram.py:22) / MelSpectrogram (no window_fn: torchaudio's default
+Hann window, prepare_spectrogram.py:27-35), power=1, normalized=True, center=True, reflect
+padding, followed by clamp((log10(S) - 1 + 5) / 5, 0, 1).  torchaudio (unpinned by the reference, absent here) is
 restated from its published algorithm; float64 rfft.  Parity: pinned against torch.stft-based
 fixtures (tests/golden/gen_golden.py --only stft), not against torchaudio itself.
 """
@@ -12,6 +13,11 @@ import numpy as np
 def hamming(n):
     k = np.arange(n, dtype=np.float64)
     return (0.54 - 0.46 * np.cos(2 * np.pi * k / n)).astype(np.float32)     # periodic=True
+
+
+def hann(n):
+    k = np.arange(n, dtype=np.float64)
+    return (0.5 - 0.5 * np.cos(2 * np.pi * k / n)).astype(np.float32)       # periodic=True
 
 
 def magnitude(audio, n_fft=1024, hop=256, window=None):
@@ -31,6 +37,9 @@ def log_features(S):
 
 
 def log_spectrogram(audio, n_fft=1024, hop=256, window=None, fb=None):
+    """fb given (mel): the window defaults to Hann, as MelSpectrogram's; else Hamming."""
+    if window is None and fb is not None:
+        window = hann(n_fft)
     S = magnitude(audio, n_fft, hop, window)
     if fb is not None:
         S = np.einsum("km,bkf->bmf", fb.astype(np.float64), S)

@@ -135,6 +135,7 @@ struct InitArgs {
 };
 hipError_t launch_init_state(const InitArgs& a, hipStream_t s);
 hipError_t launch_set_int(int* p, int v, hipStream_t s);
+hipError_t launch_delay(unsigned us, hipStream_t s);   // bounded busy wait (lane phase offsets)
 
 // ---- DiffWave (reference model/diffwave.py; diffwave.hip) ----
 struct DWEmbedArgs {          // DiffusionEmbedding + every layer's diffusion_projection, rows r = 0..R-1

@@ -523,6 +523,18 @@ hipError_t launch_set_params(StepParams* p, int t, uint64_t seed, int64_t row_of
   hipLaunchKernelGGL(set_params_kernel, dim3(1), dim3(1), 0, s, p, t, seed, row_offset);
   return hipGetLastError();
 }
+// holds a stream for `ticks` of the 100 MHz realtime counter (bounded: at most ~10^6 polls)
+__global__ void delay_kernel(unsigned ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  for (int i = 0; i < 1000000; ++i) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 >= ticks) break;
+    __builtin_amdgcn_s_sleep(8);
+  }
+}
+hipError_t launch_delay(unsigned us, hipStream_t s) {
+  hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, s, us * 100u);
+  return hipGetLastError();
+}
 hipError_t launch_set_int(int* p, int v, hipStream_t s) {
   hipLaunchKernelGGL(set_int_kernel, dim3(1), dim3(1), 0, s, p, v);
   return hipGetLastError();

@@ -1311,6 +1311,12 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
       L.g_gen = c->plan_gen;
       L.g_K = K;
     }
+    // lanes on different streams start with a phase offset (SDDM_LANE_OFFSET_US per lane index):
+    // one lane's latency-bound deep levels then overlap another lane's bandwidth-bound wide levels
+    static const int off_us = std::getenv("SDDM_LANE_OFFSET_US") ? std::atoi(std::getenv("SDDM_LANE_OFFSET_US")) : 0;
+    if (off_us > 0)
+      for (auto& Lp : c->lanes)
+        if (Lp->idx % ns) SDDM_HIP_CHECK(launch_delay((unsigned)(off_us * (Lp->idx % ns)), c->work[Lp->idx % ns]));
     for (int i = 0; i < T / K; ++i)
       for (auto& Lp : c->lanes) SDDM_HIP_CHECK(hipGraphLaunch(Lp->gexec, c->work[Lp->idx % ns]));
     for (auto& Lp : c->lanes)

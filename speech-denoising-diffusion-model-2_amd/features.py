@@ -2,7 +2,9 @@
 
 The reference computes ``torchaudio.transforms.Spectrogram(n_fft=window_length, hop_length=
 hop_samples, window_fn=torch.hamming_window, power=1, normalized=True)`` and the matching
-``MelSpectrogram(f_min=20, f_max=sr/2, n_mels, power=1, normalized=True)`` and stores
+``MelSpectrogram(f_min=20, f_max=sr/2, n_mels, power=1, normalized=True)`` -- which passes no
+window_fn, so its STFT uses torchaudio's default Hann window (prepare_spectrogram.py:27-35) --
+and stores
 ``clamp((log10(S) - 1 + 5) / 5, 0, 1)``.  torchaudio is not installed here (and its version is
 not pinned by the reference); its published algorithm is restated: torch.stft with
 ``center=True, pad_mode='reflect', onesided=True``, division by ``sqrt(sum(window**2))``
@@ -38,7 +40,8 @@ class LogSpectrogram:
 
     def __init__(self, window_length=1024, hop_samples=256, mel=False, n_mels=128, sample_rate=16000, f_min=20.0):
         self.n_fft, self.hop, self.mel = int(window_length), int(hop_samples), bool(mel)
-        self.window = torch.hamming_window(self.n_fft)
+        # '.spec.npy': Hamming (prepare_spectrogram.py:22); '.mel.npy': MelSpectrogram's default Hann
+        self.window = torch.hann_window(self.n_fft) if self.mel else torch.hamming_window(self.n_fft)
         self.fb = melscale_fbanks(self.n_fft // 2 + 1, f_min, sample_rate / 2.0, n_mels, sample_rate) if mel else None
         self.n_out = n_mels if mel else self.n_fft // 2 + 1
         self._dev = {}

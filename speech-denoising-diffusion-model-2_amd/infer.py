@@ -10,7 +10,10 @@ Differences from the reference:
       config lacks it (config_unet.json does);
   Q2  the last file of every batch is written too (the reference flushes a file only when the
       next index appears, so it drops one file per batch);
-  Q3  no DataParallel wrapper (it cannot call ``.infer``); multi-GPU runs shard rows instead;
+  Q3  no DataParallel wrapper (it cannot call ``.infer``); multi-GPU runs shard rows instead:
+      under ``torchrun --nproc-per-node P infer.py ...`` every rank samples a contiguous block of
+      each batch's rows (model.sharded_infer: row_offset-keyed noise, one RCCL all-gather), so the
+      written files equal a single-GPU run bit for bit; rank 0 writes them;
   the PESQ/STOI evaluation step needs torchmetrics (absent): the loss and SI-SNR are logged.
 """
 import argparse
@@ -63,6 +66,8 @@ def write_file(paths, name, output, target, condition, rows, datatype, sample_ra
 
 def run(config, model, loader, dataset, device, logger=None, seed=None):
     """The loop of infer.py:70-128; returns the mean loss and SI-SNR over batches."""
+    import torch.distributed as dist
+    rank = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
     datatype = dataset.datatype
     sample_rate = config["sample_rate"]
     sample_path = os.path.join(str(config.save_dir), "samples")
@@ -74,15 +79,16 @@ def run(config, model, loader, dataset, device, logger=None, seed=None):
     with torch.no_grad():
         for i, (target, condition, index) in enumerate(loader):
             target, condition = target.to(device), condition.to(device)
-            kw = {} if seed is None else {"seed": seed + i}
-            output = model.infer(condition, **kw)
+            output = module_arch.sharded_infer(model, condition, seed=None if seed is None else seed + i)
+            if rank != 0:
+                continue
             for ind, rows in regroup(index):
                 write_file(paths, dataset.getName(ind), output, target, condition, rows, datatype, sample_rate)
             total_loss += float(loss_fn(output, target))
             total_sisnr += float(module_metric.sisnr(output, target))
             n += 1
     log = {"loss": total_loss / max(n, 1), "sisnr": total_sisnr / max(n, 1)}
-    if logger:
+    if logger and rank == 0:
         logger.info(log)
     return log
 
@@ -94,10 +100,15 @@ def main(config, seed=None):
     infer_dataset = config.init_obj("infer_dataset", module_data, sample_rate=config["sample_rate"],
                                     T=config["num_samples"])
     infer_data_loader = config.init_obj("infer_data_loader", module_data, infer_dataset)
-    device = torch.device("cuda")
-    diffusion = config.init_obj("diffusion", module_diffusion, device=device)
-    network = config.init_obj("network", module_network, num_samples=config["num_samples"])
-    model = config.init_obj("arch", module_arch, diffusion, network).to(device).eval()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:                                   # torchrun: one process per GPU, RCCL over xGMI
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            dist.init_process_group("nccl")
+        torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+    device = torch.device("cuda", torch.cuda.current_device())
+    _, _, model = module_arch.build_from_config(config, module_diffusion, module_network, module_arch, device)
+    model = model.to(device).eval()
     if config.resume is not None:
         logger.info("Loading checkpoint: {} ...".format(config.resume))
         model.load_state_dict(state_dict_from_checkpoint(str(config.resume)))

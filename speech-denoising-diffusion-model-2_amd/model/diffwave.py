@@ -21,6 +21,13 @@ def Conv1d(*args, **kwargs):
     return layer
 
 
+
+def check_spectrogram(spec, bins, who):
+    """The library reads [B, bins, F] with the configured bins; a different bin count would be read
+    out of bounds.  The reference raises here too (its Conv1d(freq_bins, ...) rejects the shape)."""
+    if spec.dim() != 3 or spec.shape[1] != bins:
+        raise RuntimeError(f"{who} expects a spectrogram [B, {bins}, frames], got {tuple(spec.shape)}")
+
 class DiffusionEmbedding(nn.Module):
     def __init__(self, dim=128):
         super().__init__()
@@ -100,6 +107,7 @@ class DiffWave(nn.Module):
         if not audio.is_cuda:
             raise RuntimeError("DiffWave runs on the HIP device; move the tensors to cuda")
         spec = spectrogram.contiguous().float()
+        check_spectrogram(spec, self.freq_bins, "DiffWave")
         x = audio.contiguous().float()
         nl = diffusion_step.reshape(-1).contiguous().float()
         out = torch.empty_like(x)

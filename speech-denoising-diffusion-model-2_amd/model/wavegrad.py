@@ -17,6 +17,7 @@ import torch
 from torch import nn
 
 import sddm_hip
+from .diffwave import check_spectrogram
 
 
 class Conv1d(nn.Conv1d):
@@ -78,6 +79,7 @@ class WaveGrad(nn.Module):
     ConfigParser.init_obj adds (num_samples, freq_bins, num_timesteps) are accepted and ignored."""
 
     hop_samples = 300
+    freq_bins = 128                      # first_conv = Conv1d(128, 768, 3) (wavegrad.py:164)
 
     def __init__(self, **unused):
         super().__init__()
@@ -129,6 +131,7 @@ class WaveGrad(nn.Module):
             raise RuntimeError("WaveGrad runs on the HIP device; move the tensors to cuda")
         B = spectrogram.shape[0]
         spec = spectrogram.contiguous().float()
+        check_spectrogram(spec, self.freq_bins, "WaveGrad")
         x = audio.reshape(B, 1, -1).contiguous().float()
         nl = noise_scale.reshape(-1).contiguous().float()
         if nl.numel() != B:

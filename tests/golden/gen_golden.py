@@ -70,6 +70,10 @@ def main():
     args = ap.parse_args()
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "speech-denoising-diffusion-model-2_amd"))
+    if args.only == "stft":               # torch.stft restatement only: nothing from the reference
+        import torch
+        gen_stft(torch, args.out)
+        return
     sys.path.insert(0, args.reference)
     import torch
     torch.set_num_threads(8)
@@ -82,9 +86,6 @@ def main():
     from model.UNetModified2 import UNetModified2, PositionalEncoding
     from model.model import SDDM
     out = {}
-    if args.only == "stft":
-        gen_stft(torch, args.out)
-        return
     if args.only == "q":
         gen_q(torch, GaussianDiffusion, args.out)
         return
@@ -265,17 +266,22 @@ def gen_stft(torch, out_dir):
     audio = noisy_speech(2, 4000, seed=3).reshape(2, -1).astype(np.float32)
     audio[1, 1000:1400] = 0.0                                      # exact-zero stretch (log10(0) edge)
     x = torch.from_numpy(audio)
-    w = torch.hamming_window(1024)
-    spec = torch.stft(x, 1024, 256, 1024, w, center=True, pad_mode="reflect", normalized=False, onesided=True,
-                      return_complex=True)
-    spec = spec / w.pow(2.).sum().sqrt()
-    mag = spec.abs()
+
+    def magnitude(w):
+        spec = torch.stft(x, 1024, 256, 1024, w, center=True, pad_mode="reflect", normalized=False, onesided=True,
+                          return_complex=True)
+        return (spec / w.pow(2.).sum().sqrt()).abs()
+
+    w = torch.hamming_window(1024)                 # Spectrogram(window_fn=torch.hamming_window)
+    wm = torch.hann_window(1024)                   # MelSpectrogram: no window_fn -> torchaudio's Hann
+    mag = magnitude(w)
     fb = melscale_fbanks(513, 20.0, 8000.0, 128, 16000)
-    mel = torch.matmul(mag.transpose(-1, -2), fb).transpose(-1, -2)
+    mel = torch.matmul(magnitude(wm).transpose(-1, -2), fb).transpose(-1, -2)
     for name, S in (("spec", mag), ("mel", mel)):
         v = torch.log10(S) - 1
         st[f"stft/{name}"] = torch.clamp((v + 5) / 5, 0.0, 1.0).numpy()
     st["stft/audio"], st["stft/fb"], st["stft/window"] = audio, fb.numpy(), w.numpy()
+    st["stft/window_mel"] = wm.numpy()
     np.savez_compressed(os.path.join(out_dir, "stft.npz"), **st)
 
 

@@ -166,3 +166,29 @@ def test_reference_wavegrad_config_resolves_unchanged(tmp_path):
     lib_cfg = model.library_config()
     assert type(model).__name__ == "SDDM_spectrogram" and model.hop_samples == 300
     assert lib_cfg["network"]["type"] == "WaveGrad" and lib_cfg["diffusion"]["args"]["n_timestep"] == 1000
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference"), reason="reference configs only in the build container")
+@pytest.mark.parametrize("name,net,hop,bins", [("config_diffwave.json", "DiffWave", 256, 513),
+                                               ("config_wavegrad.json", "WaveGrad", 300, 128),
+                                               ("config_unet.json", "UNetModified2", None, None)])
+def test_reference_configs_build_unchanged(name, net, hop, bins, tmp_path):
+    """model.build_from_config resolves the reference JSONs as they are: config_diffwave.json names
+    its bins 'stft_bins'  and gives the arch no hop_samples (Q6); both come from its
+    'spectrogram' section, as train_specmodel.py:21-49 derives them."""
+    from parse_config import ConfigParser, read_json
+    import model.diffusion as module_diffusion
+    import model.model as module_arch
+    import model.network as module_network
+    cfg = read_json(os.path.join("/root/reference", name))
+    cfg["trainer"]["save_dir"] = str(tmp_path)
+    config = ConfigParser(cfg, run_id="b")
+    diffusion, network, model = module_arch.build_from_config(config, module_diffusion, module_network,
+                                                              module_arch, "cpu")
+    assert type(network).__name__ == net
+    if hop is not None:
+        assert type(model).__name__ == "SDDM_spectrogram" and model.hop_samples == hop
+        assert network.freq_bins == bins
+    lib = model.library_config()
+    assert lib["network"]["type"] == net
+    assert lib["diffusion"]["args"]["n_timestep"] == cfg["diffusion"]["args"]["n_timestep"]

@@ -111,3 +111,18 @@ def test_diffwave_config3_bench_batch(torch_cuda):
         err = rms(eps[b], ref[i])
         print(f"bf16 B=64 row {b}: rms {err:.3e}")
         assert err <= 3e-2 * max(1.0, rms(ref[i], 0))
+
+
+def test_spectrogram_bin_count_is_checked(torch_cuda):
+    """An 80-bin mel condition for a 513-bin DiffWave raises (the reference's Conv1d(freq_bins, ...)
+    rejects it) instead of being read out of bounds by the library."""
+    import model.diffusion as D
+    import model.model as M
+    n = _net()
+    spec = torch.rand(1, 80, 2, device="cuda")
+    with pytest.raises(RuntimeError):
+        n(spec, torch.zeros(1, 1, 512, device="cuda"), torch.ones(1, 1, 1, device="cuda"))
+    d = D.GaussianDiffusion("linear", 3, 1e-4, 0.05, device="cuda")
+    m = M.SDDM_spectrogram(d, n, hop_samples=256, noise_condition="time_step").cuda()
+    with pytest.raises(RuntimeError):
+        m.infer(spec, seed=1)

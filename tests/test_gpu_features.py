@@ -15,7 +15,9 @@ def test_log_spectrogram_matches_fixture(torch_cuda, mel):
     from features import LogSpectrogram
     z = golden("stft.npz")
     f = LogSpectrogram(1024, 256, mel=mel, n_mels=128, sample_rate=16000)
-    assert np.abs(f.window.numpy() - z["stft/window"]).max() == 0
+    # prepare_spectrogram.py: Hamming for the linear spectrogram, MelSpectrogram's default Hann for mel
+    assert np.abs(f.window.numpy() - z["stft/window_mel" if mel else "stft/window"]).max() == 0
+    assert np.abs(f.window.numpy() - (np.hanning(1025)[:-1] if mel else np.hamming(1025)[:-1])).max() < 1e-6
     if mel:
         assert np.abs(f.fb.numpy() - z["stft/fb"]).max() == 0
     out = f(torch.from_numpy(z["stft/audio"]).cuda()).cpu().numpy()

@@ -112,3 +112,9 @@ def test_wavegrad_bf16_bench_batch(torch_cuda):
         err = rms(eps[b], ref[i])
         print(f"bf16 B=64 row {b}: rms {err:.3e} (ref rms {rms(ref[i], 0):.3f})")
         assert err <= 3e-2 * max(1.0, rms(ref[i], 0))
+
+
+def test_wavegrad_spectrogram_bin_count_is_checked(torch_cuda):
+    n = _net()
+    with pytest.raises(RuntimeError):
+        n(torch.rand(1, 80, 2, device="cuda"), torch.zeros(1, 600, device="cuda"), torch.ones(1, device="cuda"))

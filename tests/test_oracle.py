@@ -213,7 +213,27 @@ def test_featurizer_oracle_matches_stft_fixture():
     from oracle import features as fe
     z = golden("stft.npz")
     assert np.abs(fe.hamming(1024) - z["stft/window"]).max() <= 1e-6
+    assert np.abs(fe.hann(1024) - z["stft/window_mel"]).max() <= 1e-6
     for name, fb in (("spec", None), ("mel", z["stft/fb"])):
-        out = fe.log_spectrogram(z["stft/audio"], fb=fb, window=z["stft/window"])
+        out = fe.log_spectrogram(z["stft/audio"], fb=fb)
         assert out.shape == z[f"stft/{name}"].shape
         assert np.abs(out - z[f"stft/{name}"]).max() <= 1e-5
+
+
+def test_torch_cpu_unet_matches_goldens_and_numpy_oracle():
+    """oracle/unet_torch.py (the CPU baseline bench.py times) against the reference-generated
+    forward goldens and the numpy oracle."""
+    import torch
+    from oracle import unet as ounet
+    from oracle.unet_torch import UNetTorch
+    from _helpers import golden, rms, unet_arch, unet_params
+    torch.set_num_threads(4)
+    fw = golden("unet_forward.npz")
+    for N in (2112, 16448):
+        net = UNetTorch(unet_params(N), unet_arch(N))
+        got = net(fw[f"fw/{N}/cond"], fw[f"fw/{N}/x_t"], fw[f"fw/{N}/noise_level"])
+        assert rms(got, fw[f"fw/{N}/eps"]) <= 1e-5
+    N = 2112
+    cond, x, nl = fw[f"fw/{N}/cond"], fw[f"fw/{N}/x_t"], fw[f"fw/{N}/noise_level"]
+    ref = ounet.forward(unet_params(N), unet_arch(N), cond, x, nl)
+    assert rms(UNetTorch(unet_params(N), unet_arch(N))(cond, x, nl), ref) <= 1e-5
