@@ -11,9 +11,11 @@ outputs are all-gathered over RCCL at the end of the step (weak scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--timesteps T] [--dtype bf16]
     python bench.py --workload diffwave|wavegrad     # BASELINE configs #3 / #4 (not the headline)
 
-Rank 0 prints one JSON line.  `roofline` is measured with HIP events around every conv3x3
-launch of one extra (untimed) sampling run; `cpu_baseline` times the numpy oracle on a bounded
-sample of the same workload on this host's cores.
+Rank 0 prints one JSON line.  `roofline` is the dominant kernel's (the template instantiation with
+the most time in a sampling run): algorithmic bytes per launch over its average duration, from HIP
+events around every launch of one extra (untimed) sampling run, with the whole reverse step
+reported beside it; `cpu_baseline` times a PyTorch-CPU restatement of the reference
+(oracle/unet_torch.py) at the config's batch on this host's cores.
 """
 import argparse
 import json
@@ -29,45 +31,143 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = {"bf16": 2500.0, "f16": 2500.0, "f32": 157.3}
 
 
-def cpu_baseline(B_cpu, k_steps, N, T, threads):
-    """numpy oracle (tests-only restatement of the reference) timed on the host cores."""
+def cpu_info():
+    """CPU model name and core counts of this host (the run log records them)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return model, os.cpu_count() or 1, affinity
+
+
+def cpu_baseline(B_cpu, k_steps, N, T):
+    """SURVEY §8d CPU baseline: the reference's algorithm in PyTorch CPU ops (oracle/unet_torch.py,
+    pinned to the reference goldens; tests-only restatement) at the config's batch, k reverse
+    steps timed with torch.set_num_threads(os.cpu_count()), extrapolated x T/k (every step runs
+    the same network; only t > 1 adds noise)."""
     sys.path.insert(0, REPO)
     import numpy as np
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
+    import torch
     from oracle import philox, sampler, schedule, unet
+    from oracle.unet_torch import UNetTorch
     from sddm_hip.synth import noisy_speech
     sys.path.insert(0, os.path.join(REPO, "tests"))
     from _weights import make_params, unet_shapes
+    # the host cores this process may use: OMP_NUM_THREADS where the pool sets it (the GPU box caps a
+    # job's CPU share with a quota while os.cpu_count() shows the whole machine; more threads than
+    # the quota only oversubscribe it), else every core os.cpu_count() reports
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or os.cpu_count() or 1
+    torch.set_num_threads(threads)
     arch = unet.architecture(N, inner_channel=32, channel_mults=(1, 2, 3, 4, 5), res_blocks=1)
-    P = make_params(unet_shapes(arch), 0)
+    net = UNetTorch(make_params(unet_shapes(arch), 0), arch)
     tab = schedule.make_tables("linear", T, 1e-6, 1e-3)
     cond = noisy_speech(B_cpu, N, seed=1234)
     x = sampler.get_x_T(tab, cond, philox.normal(7, 0, cond.shape))
-    unet.forward(P, arch, cond, x, np.full(B_cpu, tab["sqrt_alpha_bar"][T], np.float32))  # warm BLAS
+    net(cond, x, np.full(B_cpu, tab["sqrt_alpha_bar"][T], np.float32))                  # warm-up
     t0 = time.perf_counter()
     for i in range(k_steps):
         t = T - i
-        eps = unet.forward(P, arch, cond, x, np.full(B_cpu, tab["sqrt_alpha_bar"][t], np.float32))
+        log(f"CPU step {i + 1}/{k_steps} ({threads} threads)")
+        eps = net(cond, x, np.full(B_cpu, tab["sqrt_alpha_bar"][t], np.float32))
         x = sampler.transition("condition_in", tab, x, t, eps, cond, philox.normal(7, t, x.shape))
     dt = (time.perf_counter() - t0) / k_steps
-    return B_cpu * N / 16000.0 / (dt * T), dt
+    return B_cpu * N / 16000.0 / (dt * T), dt, threads
+
+
+def log(msg):
+    """progress on stderr (the JSON line stays the only stdout output)"""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
+def kernel_src_hash():
+    """Hash of the HIP sources: a committed PMC traffic summary is used only for the kernels it measured."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h"))):
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def unet_roofline(model, cond, N, B, T, dtype, ms_per_run):
+    """Roofline of the dominant kernel (the template instantiation with the most time in one sampling
+    run): algorithmic bytes per launch / its average launch duration, from HIP events recorded on the
+    sampling stream around every launch of one extra (untimed, non-graph) sampling run of the same
+    workload, all T steps.  The whole reverse step is reported beside it against the graph-replayed
+    wall time of the timed region.  `traffic` (PMC HBM bytes per launch) comes from the committed
+    rocprofv3 summary only when it was measured for this kernel, workload and kernel sources."""
+    import torch
+    ctx = model._context(cond.device)
+    ctx.profile(True)
+    model.infer(cond, seed=7)
+    torch.cuda.synchronize()
+    ops = ctx.profile_ops()
+    ctx.profile(False)
+    agg = {}
+    for o in ops:
+        a = agg.setdefault(o["kernel"], {"ms": 0.0, "n": 0, "bytes": 0.0, "flops": 0.0, "layers": []})
+        a["ms"] += o["avg_ms"] * o["launches"]
+        a["n"] += o["launches"]
+        a["bytes"] += o["bytes"] * o["launches"]
+        a["flops"] += o["flops"] * o["launches"]
+        a["layers"].append(o["name"])
+    total_ms = sum(a["ms"] for a in agg.values())
+    dom = max(agg, key=lambda k: agg[k]["ms"])
+    d = agg[dom]
+    avg_ms, bpl, fpl = d["ms"] / d["n"], d["bytes"] / d["n"], d["flops"] / d["n"]
+    gbs, tfs = bpl / (avg_ms * 1e-3) / 1e9, fpl / (avg_ms * 1e-3) / 1e12
+    step_bytes, step_flops = sum(o["bytes"] for o in ops), sum(o["flops"] for o in ops)
+    step_ms = ms_per_run / T
+    traffic, tsrc = None, None
+    tf = os.path.join(REPO, "profiles", "r02_hbm_traffic.json")
+    if os.path.exists(tf):
+        with open(tf) as fh:
+            pmc = json.load(fh)
+        key = {"N": N, "B": B, "dtype": dtype, "src": kernel_src_hash()}
+        if all(pmc.get(k) == v for k, v in key.items()) and dom in pmc.get("kernels", {}):
+            traffic = round(pmc["kernels"][dom]["bytes_per_launch"])
+            tsrc = "profiles/r02_hbm_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel sources and workload)"
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            "kernel": dom, "layers": d["layers"], "avg_launch_ms": round(avg_ms, 5), "launches_timed": d["n"],
+            "share_of_launch_time": round(d["ms"] / total_ms, 4), "alg_bytes_per_launch": round(bpl),
+            "mfma_tflops": round(tfs, 2), "mfma_frac": round(tfs / MFMA_PEAK_TFLOPS[dtype], 4),
+            "step": {"alg_bytes": round(step_bytes), "alg_flops": round(step_flops), "ms": round(step_ms, 5),
+                     "achieved_gbs": round(step_bytes / (step_ms * 1e-3) / 1e9, 1),
+                     "frac": round(step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                     "mfma_tflops": round(step_flops / (step_ms * 1e-3) / 1e12, 2),
+                     "launches": len(ops), "launch_time_ms": round(total_ms / T, 5)}}
 
 
 # spectrogram-conditioned workloads (BASELINE.json configs #3 and #4): config, frames, clips per GPU,
 # step-variant GFLOP per clip and step (SURVEY.md §8a rows a20 / a22)
+# (SURVEY.md §8a rows a20 / a22, §8d): step-variant GFLOP and conv-boundary elements per clip and
+# step, step-invariant elements per clip and sampling run (DiffWave's conditioner + upsampler)
 SPEC_WORKLOADS = {
     "diffwave": dict(config="config_diffwave_bench.json", frames=63, batch=64, bins=513, gflop=31.85,
+                     melems=220.9, inv_melems=319.5, bound="hbm",
                      label="DiffWave config_diffwave.json, linear 1e-4..0.02, T=200, time_step conditioning"),
     "wavegrad": dict(config="config_wavegrad_bench.json", frames=54, batch=64, bins=128, gflop=47.38,
+                     melems=92.8, inv_melems=0.0, bound="mfma",
                      label="WaveGrad, linear 1e-4..0.05, T=50 (SURVEY §8d fast schedule), sqrt_alpha_bar"),
 }
 
 
-def cpu_baseline_spec(workload, model, spec_np, T, threads):
-    """numpy oracle forward of one clip for one step, extrapolated x T (tests-only restatement)."""
+def cpu_baseline_spec(workload, model, spec_np, T):
+    """numpy oracle forward of one clip for one step (os.cpu_count() BLAS threads, set before numpy
+    is first imported by the caller's environment), extrapolated x T (tests-only restatement)."""
     sys.path.insert(0, REPO)
     import numpy as np
-    os.environ.setdefault("OMP_NUM_THREADS", str(threads))
     net = model.noise_estimate_model
     P = {k: v.detach().float().cpu().numpy() for k, v in net.state_dict().items()}
     spec = spec_np[:1]
@@ -116,25 +216,21 @@ def main_spec(args):
     hop = cfg["spectrogram"]["hop_samples"]
     N = hop * F
     torch.manual_seed(0)                                            # random-init weights
-    diffusion = config.init_obj("diffusion", module_diffusion, device=dev)
-    network = config.init_obj("network", module_network, num_samples=N, num_timesteps=T, freq_bins=W["bins"])
+    # the reference config resolves as is (model.build_from_config: SURVEY Q5 / Q6)
+    diffusion, network, model = module_arch.build_from_config(config, module_diffusion, module_network,
+                                                              module_arch, dev)
     if args.workload == "diffwave":                                 # output_projection is zero-init
         with torch.no_grad():
             network.output_projection.weight.uniform_(-0.1, 0.1)
-    extra = {} if "hop_samples" in cfg["arch"]["args"] else {"hop_samples": hop}
-    model = config.init_obj("arch", module_arch, diffusion, network, **extra).to(dev).eval()
+    model = model.to(dev).eval()
     model.compute_dtype = {"bf16": "bfloat16", "f16": "float16", "f32": "float32"}[args.dtype]
     rng = np.random.default_rng(1234)
     spec_all = rng.uniform(0, 1, (B * world, W["bins"], F)).astype(np.float32)   # U[0,1]
-    spec = torch.from_numpy(spec_all[rank * B:(rank + 1) * B]).to(dev)
-    gathered = torch.empty((B * world, 1, N), dtype=torch.float32, device=dev)
+    spec = torch.from_numpy(spec_all).to(dev)
+    result = {}
 
-    def step():
-        out = model.infer(spec, seed=7, row_offset=rank * B)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)
-        else:
-            gathered.copy_(out)
+    def step():        # the product multi-GPU path: row shards + one RCCL all-gather
+        result["out"] = module_arch.sharded_infer(model, spec, seed=7)
 
     for _ in range(args.warmup):
         step()
@@ -154,15 +250,19 @@ def main_spec(args):
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    if not torch.isfinite(gathered).all():
+    if not torch.isfinite(result["out"]).all():
         raise RuntimeError("non-finite samples")
     if rank == 0:
+        es = 2 if args.dtype != "f32" else 4
         tfs = args.steps * T * B * W["gflop"] / elapsed / 1e3      # whole-job MFMA rate per GPU
+        gbs = args.steps * B * (T * W["melems"] + W["inv_melems"]) * 1e6 * es / elapsed / 1e9
         cpu = None
         if not args.no_cpu_baseline:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-            v, dt, reps = cpu_baseline_spec(args.workload, model, spec_all, T, threads)
+            v, dt, reps = cpu_baseline_spec(args.workload, model, spec_all, T)
+            cpu_model, ncpu, naff = cpu_info()
+            threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or ncpu
             cpu = {"value": round(v, 6), "unit": "audio_s/s", "cores": threads, "kind": "port",
+                   "cpu_model": cpu_model, "cpu_count": ncpu, "cpu_affinity": naff,
                    "sample": f"numpy oracle, {reps} network evaluations of 1 clip ({dt:.2f} s each), "
                              f"extrapolated x{T} steps"}
         audio_s = args.steps * B * world * N / 16000.0
@@ -174,10 +274,16 @@ def main_spec(args):
                 "config": {"workload": f"{W['label']}, {B}x{N}-sample clips per GPU",
                            "model": network.__class__.__name__, "global_batch": B * world, "seq_len": N,
                            "timesteps": T, "parallelism": f"dp{world}"},
-                "roofline": {"bound": "mfma", "achieved": round(tfs, 2),
-                             "peak": MFMA_PEAK_TFLOPS[args.dtype], "unit": "TFLOP/s",
-                             "frac": round(tfs / MFMA_PEAK_TFLOPS[args.dtype], 4), "traffic": None,
-                             "kernel": "whole sampling run (step-variant algorithmic FLOPs / wall)"},
+                "roofline": ({"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                              "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": None,
+                              "kernel": "whole sampling run: SURVEY 8d conv-boundary bytes "
+                                        f"({W['melems']} M elements/clip/step + {W['inv_melems']} M once) / wall",
+                              "mfma_tflops": round(tfs, 2), "mfma_frac": round(tfs / MFMA_PEAK_TFLOPS[args.dtype], 4)}
+                             if W["bound"] == "hbm" else
+                             {"bound": "mfma", "achieved": round(tfs, 2), "peak": MFMA_PEAK_TFLOPS[args.dtype],
+                              "unit": "TFLOP/s", "frac": round(tfs / MFMA_PEAK_TFLOPS[args.dtype], 4), "traffic": None,
+                              "kernel": "whole sampling run (step-variant algorithmic FLOPs / wall)",
+                              "hbm_gbs": round(gbs, 1), "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}),
                 "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -194,8 +300,7 @@ def main():
     ap.add_argument("--timesteps", type=int, default=1000)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "f32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-batch", type=int, default=2)
-    ap.add_argument("--cpu-steps", type=int, default=25, help="oracle reverse steps (~10 s of host work)")
+    ap.add_argument("--cpu-steps", type=int, default=3, help="CPU reverse steps at the config's batch (extrapolated x T)")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--workload", default="unet", choices=["unet", "diffwave", "wavegrad"])
     ap.add_argument("--num-samples", type=int, default=None,
@@ -238,16 +343,13 @@ def main():
     model = config.init_obj("arch", module_arch, diffusion, network).to(dev).eval()
     model.compute_dtype = {"bf16": "bfloat16", "f16": "float16", "f32": "float32"}[args.dtype]
 
-    cond_all = noisy_speech(B * world, N, seed=1234)                 # VoiceBank-DEMAND-shaped chunks
-    cond = torch.from_numpy(cond_all[rank * B:(rank + 1) * B]).to(dev)
-    gathered = torch.empty((B * world, 1, N), dtype=torch.float32, device=dev)
+    cond_all = torch.from_numpy(noisy_speech(B * world, N, seed=1234)).to(dev)   # VoiceBank-DEMAND-shaped chunks
+    result = {}
 
     def step():
-        out = model.infer(cond, seed=7, row_offset=rank * B)
-        if world > 1:
-            dist.all_gather_into_tensor(gathered, out)              # one RCCL all-gather
-        else:
-            gathered.copy_(out)
+        # the product multi-GPU path (model.model.sharded_infer): rank r samples rows
+        # [rB, (r+1)B) with row_offset rB, then ONE RCCL all-gather of the outputs
+        result["out"] = module_arch.sharded_infer(model, cond_all, seed=7)
 
     for _ in range(args.warmup):
         step()
@@ -267,45 +369,25 @@ def main():
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
-    if not torch.isfinite(gathered).all():
+    if not torch.isfinite(result["out"]).all():
         raise RuntimeError("non-finite samples")
 
     roofline = None
-    prof = {}
+    log(f"timed region: {elapsed:.2f} s")
     if rank == 0 and not args.no_profile:
-        ctx = model._context(dev)
-        ctx.profile(True)
-        model.infer(cond, seed=7, row_offset=0)
-        torch.cuda.synchronize()
-        for cls in ("conv3x3", "gn_finalize", "final", "conv_in"):
-            prof[cls] = ctx.profile_read(cls)
-        ctx.profile(False)
-        p = prof["conv3x3"]
-        if p["launches"]:
-            gbs = p["bytes_per_launch"] / (p["avg_ms"] * 1e-3) / 1e9
-            tfs = p["flops_per_launch"] / (p["avg_ms"] * 1e-3) / 1e12
-            # measured HBM bytes per conv launch: the committed PMC summary of the same workload
-            # (tools/gpu_traffic.sh + tools/traffic.py; counters cannot be read from inside this run)
-            traffic, tsrc = None, None
-            tf = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "hbm_traffic.json")
-            if os.path.exists(tf) and (N, B, args.dtype, T) == (16448, 16, "bf16", 1000):   # the PMC workload
-                with open(tf) as fh:
-                    traffic = round(json.load(fh)["bytes_per_launch"])
-                tsrc = "profiles/hbm_traffic.json (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, same workload)"
-            roofline = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
-                        "kernel": "conv3x3_kernel (all UNet 3x3 conv launches)",
-                        "avg_launch_ms": round(p["avg_ms"], 5), "launches_timed": p["launches"],
-                        "alg_bytes_per_launch": round(p["bytes_per_launch"]),
-                        "mfma_tflops": round(tfs, 2), "mfma_frac": round(tfs / MFMA_PEAK_TFLOPS[args.dtype], 4)}
+        log("profiling one sampling run (HIP events around every launch)")
+        roofline = unet_roofline(model, cond_all[:B].contiguous(), N, B, T, args.dtype, 1e3 * elapsed / args.steps)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-        v, dt = cpu_baseline(args.cpu_batch, args.cpu_steps, N, T, threads)
+        log("CPU baseline")
+        v, dt, threads = cpu_baseline(B, args.cpu_steps, N, T)
+        cpu_model, ncpu, naff = cpu_info()
         cpu = {"value": round(v, 6), "unit": "audio_s/s", "cores": threads, "kind": "port",
-               "sample": f"numpy oracle, {args.cpu_steps} reverse steps at B={args.cpu_batch}x{N} "
-                         f"({dt:.2f} s/step), extrapolated x{T}/step"}
+               "cpu_model": cpu_model, "cpu_count": ncpu, "cpu_affinity": naff,
+               "sample": f"PyTorch-CPU restatement of UNetModified2 (oracle/unet_torch.py, pinned to the "
+                         f"reference goldens), {args.cpu_steps} reverse steps at B={B}x{N} ({dt:.2f} s/step, "
+                         f"torch.set_num_threads({threads})), extrapolated x{T}/{args.cpu_steps}"}
 
     if rank == 0:
         audio_s = args.steps * B * world * N / 16000.0
@@ -319,8 +401,6 @@ def main():
                            "model": "UNetModified2", "global_batch": B * world, "seq_len": N,
                            "timesteps": T, "parallelism": f"dp{world}"},
                 "roofline": roofline, "cpu_baseline": cpu}
-        if prof:
-            line["kernel_classes_ms"] = {k: round(v["avg_ms"], 5) for k, v in prof.items()}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -71,6 +71,7 @@ static uint16_t f32_to_f16_bits(float f) {
   return r;
 }
 static size_t dtype_size(int dt) { return dt == DT_F32 ? 4 : 2; }
+static const char* dt_name(int dt) { return dt == DT_F32 ? "f32" : dt == DT_BF16 ? "bf16" : "f16"; }
 static void store_elem(void* base, size_t idx, float v, int dt) {
   if (dt == DT_F32) ((float*)base)[idx] = v;
   else if (dt == DT_BF16) ((uint16_t*)base)[idx] = f32_to_bf16_bits(v);
@@ -207,6 +208,7 @@ struct Op {
   std::function<hipError_t(hipStream_t)> run;
   std::string name = "";
   std::function<hipError_t(hipStream_t, int)> run_dbg = nullptr;   // ablation relaunch (timing experiments)
+  std::string kname = "";   // kernel (template instantiation) the op launches, for per-kernel profiles
 };
 struct ProfAcc { double ms = 0; int64_t n = 0; double bytes = 0, flops = 0; };
 
@@ -278,11 +280,11 @@ struct sddm_ctx {
   unsigned long long* stamp_buf = nullptr;   // SDDM_STAMPS builds: phase stamps of one op
   int64_t stamp_blocks = 0;
   bool prof = false;
+  // profiling (sddm_profile_enable): HIP events around every launch, drained after each step of
+  // a lane into per-op accumulators, so every launch of a sampling run is timed with a small pool
   std::vector<hipEvent_t> ev_pool;
-  std::vector<std::pair<int, int>> ev_used;  // (op cls, pool index of start event)
-  std::vector<int> ev_op;                     // op index of each timed launch
-  std::vector<double> ev_bytes, ev_flops;
-  std::map<int, ProfAcc> prof_acc;
+  std::vector<std::pair<int, int>> ev_pend;   // (op index, pool index of the start event)
+  std::vector<ProfAcc> op_acc;                // per op index (the same layer list in every lane)
   // SDDM_spectrogram + DiffWave
   std::shared_ptr<DWState> dws;
   std::shared_ptr<WGState> wgs;
@@ -762,6 +764,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           x.cond = lp->rs.cond; x.x = lp->rs.x; x.t_dev = lp->rs.t_dev;
                           return launch_conv_in(dt, x, B, s);
                         }, "downs.0"});
+      L.ops.back().kname = std::string("conv_in_kernel<") + dt_name(dt) + ">";
     } else if (st.type == ST_CONV) {
       ConvArgs a{};
       const Tensor sa = TT(st.srcA), sb = TT(st.srcB), o = TT(st.out);
@@ -828,6 +831,18 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           x.ck_batch = ch.ckb; x.deep_nw = ch.nw;
                           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
                         }, st.w + (ch.strip ? "[strip]" : (ch.tile >= 0 ? "[tile" + std::to_string(ch.tile) + "]" : ""))});
+      {
+        char kn[160];
+        if (ch.strip)
+          snprintf(kn, sizeof(kn), "conv_strip_kernel<%s,%d,%d,%d,%d>", dt_name(dt), ch.nblk / 16, a.Wo, Cin, ch.mpi);
+        else if (ch.tile >= 0) {
+          const TileCfg tc = conv_tile_cfg(ch.tile);
+          snprintf(kn, sizeof(kn), "conv_tile_kernel<%s,%d,%d,%d,%d,%d> (tile%d)", dt_name(dt), s2 ? 1 : 0, tc.wpx, tc.wco,
+                   tc.fp, tc.fc, ch.tile);
+        } else
+          snprintf(kn, sizeof(kn), "conv_deep_kernel<%s,%d,%d,%d>", dt_name(dt), s2 ? 1 : 0, ch.mt, ch.nw);
+        L.ops.back().kname = kn;
+      }
       {  // flags: 1 no stats, 2 no GroupNorm transform, 4 no residual / embedding, 8 skip the K loop
         auto base = L.ops.back().run;
         ConvArgs a0 = a;
@@ -879,6 +894,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           x.sp = lp->rs.t_dev ? (const StepParams*)lp->rs.t_dev : nullptr;
                           return launch_final(dt, x, B, s);
                         }, "final_conv"});
+      L.ops.back().kname = std::string("final_kernel<") + dt_name(dt) + ">";
     }
   }
   return SDDM_OK;
@@ -926,12 +942,26 @@ static int ensure_ready(sddm_ctx* c) {
   return SDDM_OK;
 }
 
+static int prof_drain(sddm_ctx* c, const Lane& L) {
+  if (c->ev_pend.empty()) return SDDM_OK;
+  SDDM_HIP_CHECK(hipEventSynchronize(c->ev_pool[c->ev_pend.back().second + 1]));
+  if (c->op_acc.size() < L.ops.size()) c->op_acc.resize(L.ops.size());
+  for (const auto& pe : c->ev_pend) {
+    float m = 0;
+    SDDM_HIP_CHECK(hipEventElapsedTime(&m, c->ev_pool[pe.second], c->ev_pool[pe.second + 1]));
+    ProfAcc& a = c->op_acc[pe.first];
+    a.ms += m; a.n += 1; a.bytes += L.ops[pe.first].bytes; a.flops += L.ops[pe.first].flops;
+  }
+  c->ev_pend.clear();
+  return SDDM_OK;
+}
+
 static int run_ops(sddm_ctx* c, Lane& L, hipStream_t s) {
   for (const Op& op : L.ops) {
-    const bool timed = c->prof && (size_t)(c->ev_used.size() * 2 + 2) <= c->ev_pool.size();
+    const bool timed = c->prof && c->ev_pend.size() * 2 + 2 <= c->ev_pool.size();
     int e0 = 0;
     if (timed) {
-      e0 = (int)c->ev_used.size() * 2;
+      e0 = (int)c->ev_pend.size() * 2;
       SDDM_HIP_CHECK(hipEventRecord(c->ev_pool[e0], s));
     }
     hipError_t e = op.run(s);
@@ -946,12 +976,10 @@ static int run_ops(sddm_ctx* c, Lane& L, hipStream_t s) {
     }
     if (timed) {
       SDDM_HIP_CHECK(hipEventRecord(c->ev_pool[e0 + 1], s));
-      c->ev_used.push_back({op.cls, e0});
-      c->ev_op.push_back((int)(&op - L.ops.data()));
-      c->ev_bytes.push_back(op.bytes);
-      c->ev_flops.push_back(op.flops);
+      c->ev_pend.push_back({(int)(&op - L.ops.data()), e0});
     }
   }
+  if (c->prof) return prof_drain(c, L);
   return SDDM_OK;
 }
 
@@ -1507,12 +1535,18 @@ int sddm_profile_enable(sddm_ctx* c, int enable) {
   if (!c) FAIL(SDDM_ERR_INVALID_ARG, "NULL ctx");
   SDDM_HIP_CHECK(hipSetDevice(c->device));
   c->prof = enable != 0;
-  c->ev_used.clear(); c->ev_bytes.clear(); c->ev_flops.clear(); c->prof_acc.clear(); c->ev_op.clear();
+  c->ev_pend.clear();
+  c->op_acc.clear();
   if (c->prof && c->ev_pool.empty()) {
-    c->ev_pool.resize(20000);
+    c->ev_pool.resize(512);
     for (auto& e : c->ev_pool) SDDM_HIP_CHECK(hipEventCreate(&e));
   }
   return SDDM_OK;
+}
+
+static const std::vector<Op>& profiled_ops(sddm_ctx* c) {
+  static const std::vector<Op> kNoOps;
+  return c->lanes.empty() ? kNoOps : c->lanes[0]->ops;   // the same layer list in every lane
 }
 
 int sddm_profile_read(sddm_ctx* c, const char* kernel_class, double* avg_ms, int64_t* launches,
@@ -1521,16 +1555,12 @@ int sddm_profile_read(sddm_ctx* c, const char* kernel_class, double* avg_ms, int
   const std::string k = kernel_class;
   const int cls = k == "conv_in" ? 0 : k == "gn_finalize" ? 1 : k == "conv3x3" ? 2 : k == "final" ? 3 : -1;
   if (cls < 0) FAIL(SDDM_ERR_INVALID_ARG, "kernel class %s", kernel_class);
-  SDDM_HIP_CHECK(hipSetDevice(c->device));
+  const std::vector<Op>& ops = profiled_ops(c);
   double ms = 0, bytes = 0, flops = 0;
   int64_t n = 0;
-  for (size_t i = 0; i < c->ev_used.size(); ++i) {
-    if (c->ev_used[i].first != cls) continue;
-    const int e0 = c->ev_used[i].second;
-    SDDM_HIP_CHECK(hipEventSynchronize(c->ev_pool[e0 + 1]));
-    float m = 0;
-    SDDM_HIP_CHECK(hipEventElapsedTime(&m, c->ev_pool[e0], c->ev_pool[e0 + 1]));
-    ms += m; bytes += c->ev_bytes[i]; flops += c->ev_flops[i]; ++n;
+  for (size_t i = 0; i < c->op_acc.size() && i < ops.size(); ++i) {
+    if (ops[i].cls != cls) continue;
+    ms += c->op_acc[i].ms; bytes += c->op_acc[i].bytes; flops += c->op_acc[i].flops; n += c->op_acc[i].n;
   }
   if (avg_ms) *avg_ms = n ? ms / n : 0.0;
   if (launches) *launches = n;
@@ -1556,24 +1586,16 @@ int sddm_debug_stamps(sddm_ctx* c, void* host, int64_t max_blocks, int64_t* n_bl
 
 int sddm_profile_ops(sddm_ctx* c, char* buf, int64_t buflen) {
   if (!c || !buf || buflen < 3) FAIL(SDDM_ERR_INVALID_ARG, "NULL argument");
-  SDDM_HIP_CHECK(hipSetDevice(c->device));
-  static const std::vector<Op> kNoOps;
-  const std::vector<Op>& ops = c->lanes.empty() ? kNoOps : c->lanes[0]->ops;   // same layer list in every lane
-  std::vector<double> ms(ops.size(), 0.0);
-  std::vector<int64_t> n(ops.size(), 0);
-  for (size_t i = 0; i < c->ev_used.size(); ++i) {
-    const int e0 = c->ev_used[i].second, op = c->ev_op[i];
-    SDDM_HIP_CHECK(hipEventSynchronize(c->ev_pool[e0 + 1]));
-    float m = 0;
-    SDDM_HIP_CHECK(hipEventElapsedTime(&m, c->ev_pool[e0], c->ev_pool[e0 + 1]));
-    if (op >= 0 && op < (int)ms.size()) { ms[op] += m; ++n[op]; }
-  }
+  const std::vector<Op>& ops = profiled_ops(c);
   std::string js = "[";
-  char tmp[512];
+  char tmp[768];
   for (size_t i = 0; i < ops.size(); ++i) {
-    snprintf(tmp, sizeof(tmp), "%s{\"name\": \"%s\", \"cls\": %d, \"launches\": %lld, \"avg_ms\": %.6f, \"bytes\": %.0f, \"flops\": %.0f}",
-             i ? ", " : "", ops[i].name.c_str(), ops[i].cls, (long long)n[i], n[i] ? ms[i] / n[i] : 0.0,
-             ops[i].bytes, ops[i].flops);
+    const ProfAcc a = i < c->op_acc.size() ? c->op_acc[i] : ProfAcc{};
+    snprintf(tmp, sizeof(tmp),
+             "%s{\"name\": \"%s\", \"kernel\": \"%s\", \"cls\": %d, \"launches\": %lld, \"avg_ms\": %.6f, "
+             "\"bytes\": %.0f, \"flops\": %.0f}",
+             i ? ", " : "", ops[i].name.c_str(), ops[i].kname.c_str(), ops[i].cls, (long long)a.n,
+             a.n ? a.ms / a.n : 0.0, ops[i].bytes, ops[i].flops);
     js += tmp;
   }
   js += "]";
