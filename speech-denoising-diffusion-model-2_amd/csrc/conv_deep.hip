@@ -198,11 +198,14 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   const int ns3 = nck * 9, ns = ns3 + rck;
   const int nj = wv < ns ? (ns - wv + NW - 1) / NW : 0;
   const int s_last = wv + NW * max(nj - 1, 0);
-  const size_t w3 = (size_t)nck * 9 * 32;                // elements per packed 3x3 weight row
-  const T* wbase = (const T*)a.wgt + (size_t)(n0 + (lane & 15)) * w3 + g * 8;
-  const T* rbase = (const T*)a.res_wgt + (size_t)(n0 + (lane & 15)) * RC + g * 8 - (size_t)ns3 * 32;
+  // weights in MFMA-fragment order (ConvArgs::wgt_f): the 64 lanes of one A fragment read one
+  // contiguous 1 KiB (bf16 / f16) or 2 KiB (fp32) run, not 16 rows x 64 B pieces
+  const int cb0 = n0 / 16;
+  const T* wbase = (const T*)a.wgt_f + (size_t)lane * 8;
+  const T* rbase = (const T*)a.res_wgt_f + (size_t)lane * 8;
   auto wfrag = [&](int s, int fc) -> Frag<T> {
-    const T* p = s < ns3 ? wbase + (size_t)fc * 16 * w3 + (size_t)s * 32 : rbase + (size_t)fc * 16 * RC + (size_t)s * 32;
+    const T* p = s < ns3 ? wbase + ((size_t)(cb0 + fc) * ns3 + s) * 512
+                         : rbase + ((size_t)(cb0 + fc) * rck + (s - ns3)) * 512;
     return load_frag<T>((const char*)p);
   };
   Frag<T> wa[D][FC];

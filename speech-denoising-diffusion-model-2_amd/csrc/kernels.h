@@ -78,6 +78,10 @@ struct ConvArgs {
   // one output channel: 3x3 [Cin/32][9][4][Cout][8], res_conv [RC/32][4][Cout][8]
   const void* wgt_t;
   const void* res_wgt_t;
+  // conv_deep: MFMA-fragment-major weight images, one 64-lane A fragment contiguous:
+  // 3x3 [Cout/16][Cin/32 * 9][64 lanes][8], res_conv [Cout/16][RC/32][64 lanes][8]
+  const void* wgt_f;
+  const void* res_wgt_f;
 };
 
 // ---- K-streamed implicit-GEMM tile convolution (conv_tile.hip, bf16 / f16 only) ----

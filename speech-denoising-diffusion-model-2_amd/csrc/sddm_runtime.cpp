@@ -343,6 +343,22 @@ static int upload_weights(sddm_ctx* c) {
     b.off = A.reserve(b.bytes.size());
     c->woff[name] = b.off;
     blobs.push_back(std::move(b));
+    {  // conv_deep fragment image [co/16][ci/32 * 9][64 lanes][8]: lane l of step s holds
+       // W[16 cb + (l & 15)][32 (s / 9) + 8 (l >> 4) + j][tap s % 9]
+      Blob bf;
+      const int ns = (ci / 32) * 9;
+      bf.bytes.assign((size_t)co * ci * 9 * es, 0);
+      for (int o = 0; o < co; ++o)
+        for (int i = 0; i < ci; ++i)
+          for (int tap = 0; tap < 9; ++tap) {
+            const int s = (i / 32) * 9 + tap, l = (o % 16) + 16 * ((i % 32) / 8);
+            const size_t dst = (((size_t)(o / 16) * ns + s) * 64 + l) * 8 + i % 8;
+            store_elem(bf.bytes.data(), dst, w.data[((size_t)o * ci + i) * 9 + tap], dt);
+          }
+      bf.off = A.reserve(bf.bytes.size());
+      c->woff[name + "_f"] = bf.off;
+      blobs.push_back(std::move(bf));
+    }
     if (dt != DT_F32) {  // conv_tile image [ci/32][9][4][co][8]: one 16-byte unit = 8 input channels
       Blob bt;
       bt.bytes.assign((size_t)co * ci * 9 * es, 0);
@@ -367,6 +383,19 @@ static int upload_weights(sddm_ctx* c) {
     b.off = A.reserve(b.bytes.size());
     c->woff[name] = b.off;
     blobs.push_back(std::move(b));
+    {  // conv_deep fragment image [co/16][ci/32][64 lanes][8]
+      Blob bf;
+      bf.bytes.assign((size_t)co * ci * es, 0);
+      for (int o = 0; o < co; ++o)
+        for (int i = 0; i < ci; ++i) {
+          const int l = (o % 16) + 16 * ((i % 32) / 8);
+          store_elem(bf.bytes.data(), (((size_t)(o / 16) * (ci / 32) + i / 32) * 64 + l) * 8 + i % 8,
+                     w.data[(size_t)o * ci + i], dt);
+        }
+      bf.off = A.reserve(bf.bytes.size());
+      c->woff[name + "_f"] = bf.off;
+      blobs.push_back(std::move(bf));
+    }
     if (dt != DT_F32) {  // conv_tile image [ci/32][4][co][8]
       Blob bt;
       bt.bytes.assign((size_t)co * ci * es, 0);
@@ -783,6 +812,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       }
       a.wgt = WV(st.w + ".w"); a.bias = WF(st.w + ".b");
       a.wgt_t = c->woff.count(st.w + ".w_t") ? WV(st.w + ".w_t") : nullptr;
+      a.wgt_f = WV(st.w + ".w_f");
       a.res_mode = st.res_mode;
       const int Cin = a.CA + a.CB;
       double bytes = (double)B * a.Hi * a.Wi * Cin * es + (double)B * a.Ho * a.Wo * a.Cout * es +
@@ -796,6 +826,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         a.rawA = ra.p; a.rawB = rb.p; a.RCA = ra.C; a.RCB = rb.C;
         a.res_wgt = WV(st.rb + ".res.w");
         a.res_wgt_t = c->woff.count(st.rb + ".res.w_t") ? WV(st.rb + ".res.w_t") : nullptr;
+        a.res_wgt_f = WV(st.rb + ".res.w_f");
         if ((ra.C + rb.C) % 32) FAIL(SDDM_ERR_SHAPE, "%s.res_conv: channels must be multiples of 32", st.rb.c_str());
         bytes += (double)B * a.Ho * a.Wo * (ra.C + rb.C) * es + (double)a.Cout * (ra.C + rb.C) * es;
         flops += 2.0 * B * a.Ho * a.Wo * a.Cout * (double)(ra.C + rb.C);
