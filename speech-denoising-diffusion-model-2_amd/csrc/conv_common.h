@@ -69,6 +69,17 @@ template <> __device__ __forceinline__ void store4<bf16_t>(bf16_t* p, float a, f
 template <> __device__ __forceinline__ void store4<f16_t>(f16_t* p, float a, float b, float c, float d) {
   *(f16x4*)p = f16x4{(f16_t)a, (f16_t)b, (f16_t)c, (f16_t)d};
 }
+// the same from two packed pairs (the accumulator register pairs): one v_cvt_pk per pair
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <typename T> __device__ __forceinline__ void store4p(T* p, f32x2 a, f32x2 b) { store4<T>(p, a.x, a.y, b.x, b.y); }
+template <> __device__ __forceinline__ void store4p<bf16_t>(bf16_t* p, f32x2 a, f32x2 b) {
+  typedef bf16_t bf16x2_t __attribute__((ext_vector_type(2)));
+  typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+  const bf16x2_t x = __builtin_convertvector(a, bf16x2_t), y = __builtin_convertvector(b, bf16x2_t);
+  *(u32x2_t*)p = u32x2_t{__builtin_bit_cast(unsigned int, x), __builtin_bit_cast(unsigned int, y)};
+}
+// bf16 / f16 / f32 pair -> two floats
+template <typename T> __device__ __forceinline__ f32x2 unpack2(T a, T b) { return f32x2{to_f32<T>(a), to_f32<T>(b)}; }
 template <typename T> __device__ __forceinline__ f32x4 load4(const T* p);
 template <> __device__ __forceinline__ f32x4 load4<float>(const float* p) { return *(const f32x4*)p; }
 template <> __device__ __forceinline__ f32x4 load4<bf16_t>(const bf16_t* p) {
@@ -317,8 +328,6 @@ namespace sddm {
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 __device__ __forceinline__ float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
-
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // SiLU of two values with packed fp32 arithmetic around the two transcendentals per value:
 // y * 1 / (1 + 2^(-y log2 e))

@@ -240,7 +240,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   SDDM_STAMP(a, 3);
   // bias + noise embedding of this thread's 4 epilogue channels: in flight during the K loop
   const int ec4 = (tid & 7) * 4;
-  float bb[4];
+  float bb[4], sshift;
   {
     const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
 #pragma unroll
@@ -248,6 +248,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
       const float bv = a.bias[n0 + ec4 + i], tv = trow[n0 + ec4 + i];
       bb[i] = bv + (a.temb ? tv : 0.f);
     }
+    const int cs = n0 + (tid & (NB - 1));                // statistics shift of channel n0 + tid (tid < NB)
+    const float sbv = a.bias[cs], stv = trow[cs];
+    sshift = sbv + (a.temb ? stv : 0.f);
   }
 
   // ---------------- 3. this wave's K steps ----------------
@@ -379,8 +382,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
         const float* e = xs + (r * NB + tid) * 3;
         n += e[0]; u1 += e[1]; u2 += e[2];
       }
-      const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : nullptr;
-      const float shift = a.bias[n0 + tid] + (trow ? trow[n0 + tid] : 0.f);
+      const float shift = sshift;
       float* dst = a.stats + (((size_t)b * a.n_tiles + tile) * a.Cout + n0 + tid) * 2;
       dst[0] = (shift + u1 / n) * n;
       dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);

@@ -1,394 +1,15 @@
-// Row-streaming ("line buffer") 3x3 convolution for the wide UNet levels (segment width W = 128
-// and 64: UNetModified2 levels 0-1, where >60 % of the FLOPs live).
-//
-// One block owns image b, output channels [n0, n0 + 16*FC) and a strip of SR output rows.  It
-// keeps in LDS
-//   * the weight slab of its channel tile (loaded once per strip, not once per tile), and
-//   * a ring of R = 2*TR + 2 transformed input rows (GroupNorm + SiLU applied once per element,
-//     zero halo columns, nearest-2x upsample / channel concat resolved while loading),
-// and walks the strip TR = MPI / W output rows at a time (MPI = 128 or 256 pixels, one wave per
-// 32 pixels = 2 MFMA column fragments; with MPI = 256 each SIMD runs two waves, so one wave's
-// GN+SiLU staging overlaps the other's MFMAs).  While the MFMAs of iteration i run on rows [y-1, y+TR] of the ring, each thread
-// already holds in registers the raw input of rows [y+TR+1, y+2TR] (issued before the MFMAs) and
-// writes them transformed into the free ring slots afterwards: one barrier per iteration.
-//
-// LDS images are plane-major (a plane = one 16-byte channel unit of every pixel / output channel,
-// plane stride = 0 mod 256 B): the 16 lanes of an MFMA operand read 16 consecutive 16-byte slots
-// and the ds_read_b128 lane groups never collide; staging writes go 8 consecutive pixels per
-// 8-lane group (conflict free) while the 64 lanes of a wave read 64/UPP whole pixels (coalesced).
-// Geometry (W, Cin) is compile-time so no integer division runs per element.
-// The epilogue adds bias, the noise-embedding projection and the residual (identity, or the
-// ResnetBlock 1x1 res_conv as extra MFMAs on raw input fragments loaded straight to registers),
-// stores 4 channels per lane, and accumulates GroupNorm statistics of the fp32 values in
-// registers (per-lane shifted sums, merged with Chan's formula at the end of the strip).
-#include "conv_common.h"
+// Row-streaming 3x3 convolution: host entry points (kernel in conv_strip_impl.h, instantiated per
+// storage type in conv_strip_{bf16,f16,f32}.hip).
 #include "kernels.h"
+#include "sddm_common.h"
 
 namespace sddm {
 
-template <typename T, int FC, int W, int CIN, int MPI>
-__global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR) {
-  constexpr int NT = MPI * 2;                     // threads: one wave per 32 pixels of an iteration
-  constexpr int NWV = NT / 64;
-  constexpr int ES = (int)sizeof(T);
-  constexpr int NBLK = 16 * FC, FP = 2;
-  constexpr int TR = MPI / W, R = 2 * TR + 2;
-  constexpr int UPP = CIN * ES / 16;              // 16-byte channel units (planes) per pixel
-  constexpr int UPL = ES / 2;                     // units per lane group (8 channels)
-  constexpr int VE = 16 / ES;
-  constexpr int PL = ((W + 2) * 16 + 255) / 256 * 256;
-  constexpr int SLOT = UPP * PL;
-  constexpr int NCK = CIN / 32;
-  constexpr int WPL = NBLK * 16;                  // weight plane stride
-  constexpr int WPLANES = NCK * 9 * 4 * UPL;
-  constexpr int PB = 64 / UPP;                    // pixels per 64-unit staging group
-  constexpr int NU = TR * W * UPP;                // units of TR rows
-  constexpr int UPT = NU / NT;                    // prefetch units per thread and row group
-  constexpr int IU = ((TR + 2) * W * UPP + NT - 1) / NT;   // initial-row units per thread
-  constexpr int RCKM = 4;                         // res_conv chunks held in registers (RC <= 128)
-  static_assert(UPP >= 1 && UPP <= 64 && (64 % UPP) == 0, "channel units must divide a wave");
-  static_assert(NU % NT == 0, "prefetch must split evenly");
-  typedef T vec4 __attribute__((ext_vector_type(4)));
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int strip = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NBLK;
-  const int H = a.Ho;
-  const int RC = a.RCA + a.RCB;
-  const int rck = a.res_mode == 2 ? RC / 32 : 0;
-  const bool gn = a.gamma != nullptr;
-
-  char* ring = smem;                              // [R][UPP planes][PL]
-  char* wl = ring + R * SLOT;                     // [WPLANES][NBLK][16 B]
-  char* rw = wl + WPLANES * WPL;                  // [RC*ES/16 planes][NBLK][16 B]
-  const int RPLANES = rck * 32 * ES / 16;
-  float* gsc = (float*)(rw + RPLANES * WPL);      // [2][CIN]
-  float* red = gsc + 2 * CIN;                     // [NWV waves][NBLK][3]
-
-  const int y0 = strip * SR;
-  const int iters = SR / TR;
-  SDDM_STAMP(a, 0);
-  // ---------------- prologue: every independent load issued before anything waits ----------------
-  GNLoad gl;
-  const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
-  // initial ring rows y0-1 .. y0+TR (raw), clamped addresses, zero rows outside the image later
-  const T* srcAb = (const T*)a.srcA + (size_t)b * a.Hi * a.Wi * a.CA;
-  const T* srcBb = a.CB ? (const T*)a.srcB + (size_t)b * a.Hi * a.Wi * a.CB : srcAb;
-  f32x4 ini[IU];
-#pragma unroll
-  for (int k = 0; k < IU; ++k) {
-    const int u = min(tid + k * NT, (TR + 2) * W * UPP - 1);
-    const int grp = u >> 6, j = u & 63;
-    const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
-    const int ry = min(max(y0 - 1 + r, 0), H - 1);
-    const int sy = a.upsample ? ry >> 1 : ry, sx = a.upsample ? x >> 1 : x;
-    const int c0 = q * VE;
-    const bool fa = c0 < a.CA;
-    ini[k] = *(const f32x4*)((fa ? srcAb : srcBb) + ((size_t)sy * a.Wi + sx) * (fa ? a.CA : a.CB) + (fa ? c0 : c0 - a.CA));
-  }
-  // weight slabs straight into LDS (LDS-DMA: unit u lands at byte 16 u, co fastest, so every
-  // wave-instruction fills 1 KiB of consecutive LDS; no VGPRs, no wait until the first barrier)
-  // NBLK * WPLANES and NBLK * RPLANES are multiples of 64: whole waves, no tail
-  for (int u0 = wave * 64; u0 < NBLK * WPLANES; u0 += NT) {
-    const int u = u0 + lane;
-    const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
-    const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
-    const char* src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(wl + u0 * 16), 16, 0, 0);
-  }
-  for (int u0 = wave * 64; u0 < NBLK * RPLANES; u0 += NT) {
-    const int u = u0 + lane;
-    const int co = u % NBLK, pl = u / NBLK;
-    const char* src = (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(rw + u0 * 16), 16, 0, 0);
-  }
-  for (int u = tid; u < R * UPP * 2; u += NT) {           // zero halo columns
-    const int side = u & 1, pl = u >> 1;
-    *(f32x4*)(ring + pl * PL + (side ? (W + 1) : 0) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + CIN);
-  __syncthreads();                                         // gsc ready
-  // bias + noise embedding of this lane's epilogue channels: unconditional loads at clamped
-  // channels (a load under a condition is waited for at the branch join), issued before the
-  // initial ring commit so they are in flight during its GroupNorm + SiLU work
-  const int t_now = a.t_dev ? *a.t_dev : 0;
-  const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
-  float badd[FC][4];
-#pragma unroll
-  for (int fc = 0; fc < FC; ++fc)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int co = n0 + fc * 16 + 4 * g + i, cc = min(co, a.Cout - 1);
-      const float bv = a.bias[cc], tv = trow[cc];
-      badd[fc][i] = (co < a.Cout) ? bv + (a.temb ? tv : 0.f) : 0.f;
-    }
-  const int base = ((y0 - 1) % R + R) % R;                 // ring slot of row y0 - 1
-#pragma unroll
-  for (int k = 0; k < IU; ++k) {
-    const int u = tid + k * NT;
-    if (u >= (TR + 2) * W * UPP) break;
-    const int grp = u >> 6, j = u & 63;
-    const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
-    const int ry = y0 - 1 + r;
-    f32x4 v = ini[k];
-    if (ry < 0 || ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
-    else if (gn) v = transform_fast<T>(v, gsc + q * VE, gsc + CIN + q * VE);
-    *(f32x4*)(ring + ((base + r) % R) * SLOT + q * PL + (x + 1) * 16) = v;
-  }
-
-  int prow[FP], pcol[FP];
-#pragma unroll
-  for (int fp = 0; fp < FP; ++fp) {
-    const int p = wave * 32 + fp * 16 + (lane & 15);   // pixel inside the MPI-pixel iteration
-    prow[fp] = p / W;
-    pcol[fp] = p % W;
-  }
-  // row-group prefetch geometry of this thread's units (the same every iteration), and the
-  // GroupNorm scale / shift of their channels held in registers
-  // (all per-iteration address math below is 32-bit with 24-bit multiplies: full-rate VALU)
-  int pr[UPT], uoff[UPT], loff[UPT], cq[UPT];  // row in group, source offset (elements, +A/B flag), LDS offset, channel
-#pragma unroll
-  for (int k = 0; k < UPT; ++k) {
-    const int u = tid + k * NT, grp = u >> 6, j = u & 63;
-    const int pix = grp * PB + (j % PB);
-    const int q = j / PB, x = pix % W;
-    pr[k] = pix / W;
-    loff[k] = q * PL + (x + 1) * 16;
-    cq[k] = q * VE;
-    const int c0 = q * VE;
-    const int sx = a.upsample ? (x >> 1) : x;
-    const bool fa = c0 < a.CA;
-    uoff[k] = (fa ? sx * a.CA + c0 : sx * a.CB + (c0 - a.CA)) * 2 + (fa ? 0 : 1);
-  }
-  const int rsA = a.Wi * a.CA, rsB = a.Wi * a.CB;          // elements per source row
-  // rows of row group j (written to the ring at the end of iteration j-1, read by iteration j)
-  auto issue_rows = [&](f32x4 (&dst)[UPT], int j) {
-#pragma unroll
-    for (int k = 0; k < UPT; ++k) {
-      const int ry = min(y0 + j * TR + 1 + pr[k], H - 1);
-      const int sy = a.upsample ? (ry >> 1) : ry;
-      const bool fb = uoff[k] & 1;
-      dst[k] = *(const f32x4*)((fb ? srcBb : srcAb) + ((uoff[k] >> 1) + (int)__umul24(sy, fb ? rsB : rsA)));
-    }
-  };
-  auto commit_rows = [&](const f32x4 (&src)[UPT], int j) {
-    const int sb = (base + j * TR + 2) % R;             // uniform
-#pragma unroll
-    for (int k = 0; k < UPT; ++k) {
-      const int ry = y0 + j * TR + 1 + pr[k];
-      f32x4 v = src[k];
-      if (ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
-      else if (gn && !(a.dbg & 2)) v = transform_lds<T>(v, gsc + cq[k], gsc + CIN + cq[k]);
-      int sl = sb + pr[k];
-      sl = sl >= R ? sl - R : sl;
-      *(f32x4*)(ring + (int)__umul24(sl, SLOT) + loff[k]) = v;
-    }
-  };
-  // residual inputs of iteration it (issued one iteration ahead)
-  const T* resb = a.res_mode == 1 ? (const T*)a.res_src + (size_t)b * H * W * a.Cout : nullptr;
-  auto issue_res1 = [&](vec4 (&dst)[FP][FC], int it) {
-#pragma unroll
-    for (int fp = 0; fp < FP; ++fp) {
-      const int yy = min(y0 + it * TR, H - TR) + prow[fp];
-      const int po = (int)__umul24(yy * W + pcol[fp], a.Cout);
-#pragma unroll
-      for (int fc = 0; fc < FC; ++fc) {
-        const int co = min(n0 + fc * 16 + 4 * g, a.Cout - 4);
-        dst[fp][fc] = *(const vec4*)(resb + (po + co));
-      }
-    }
-  };
-  const T* rawAb = rck ? (const T*)a.rawA + (size_t)b * H * W * a.RCA : nullptr;
-  const T* rawBb = (rck && a.RCB) ? (const T*)a.rawB + (size_t)b * H * W * a.RCB : rawAb;
-  auto issue_res2 = [&](Frag<T> (&dst)[RCKM][FP], int it) {
-#pragma unroll
-    for (int ck = 0; ck < RCKM; ++ck)
-#pragma unroll
-      for (int fp = 0; fp < FP; ++fp) {
-        const int yy = min(y0 + it * TR, H - TR) + prow[fp];
-        const int c0 = min(ck, rck - 1) * 32 + g * 8;
-        const int pix = yy * W + pcol[fp];
-        const T* sp = c0 < a.RCA ? rawAb + ((int)__umul24(pix, a.RCA) + c0) : rawBb + ((int)__umul24(pix, a.RCB) + (c0 - a.RCA));
-        dst[ck][fp] = load_frag<T>((const char*)sp);
-      }
-  };
-
-  float s1[FC][4], s2[FC][4];                  // sums of (value - badd): shift = bias + embedding
-#pragma unroll
-  for (int fc = 0; fc < FC; ++fc)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { s1[fc][i] = 0.f; s2[fc][i] = 0.f; }
-  T* outb = (T*)a.out + (size_t)b * H * W * a.Cout;
-  const char* abase = wl + g * UPL * WPL + (lane & 15) * 16;
-  const char* rbase = rw + g * UPL * WPL + (lane & 15) * 16;
-
-  // one iteration: MFMAs on the ring rows of row group it, epilogue, ring refill with row group
-  // it+1 (loaded two iterations earlier); the loads of row group it+3 are issued at the top
-  f32x4 rowsA[UPT], rowsB[UPT], rowsC[UPT];
-  vec4 r1A[FP][FC], r1B[FP][FC];
-  auto body = [&](int it, f32x4 (&nxt)[UPT], f32x4 (&fill)[UPT], vec4 (&r1cur)[FP][FC], vec4 (&r1nxt)[FP][FC]) {
-    const int y = y0 + it * TR;
-    const int s_it = (base + it * TR) % R;               // slot of row y - 1
-    issue_rows(nxt, it + 3);
-    if (a.res_mode == 1) issue_res1(r1nxt, it + 1);
-    Frag<T> r2cur[RCKM][FP];
-    if (rck) issue_res2(r2cur, it);                      // consumed after the 3x3 MFMAs
-    f32x4 acc[FP][FC];
-#pragma unroll
-    for (int i = 0; i < FP; ++i)
-#pragma unroll
-      for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const char* bptr[FP][3];
-#pragma unroll
-    for (int fp = 0; fp < FP; ++fp)
-#pragma unroll
-      for (int dy = 0; dy < 3; ++dy) {
-        int sl = s_it + prow[fp] + dy;                   // < 2R: one conditional wrap
-        sl = sl >= R ? sl - R : sl;
-        bptr[fp][dy] = ring + (int)__umul24(sl, SLOT) + g * UPL * PL + pcol[fp] * 16;
-      }
-#pragma unroll
-    for (int ck = 0; ck < NCK; ++ck) {
-      if (a.dbg & 8) break;
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int dy = tap / 3, dx = tap - 3 * dy;
-        Frag<T> bf[FP];
-#pragma unroll
-        for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(bptr[fp][dy] + ck * 4 * UPL * PL + dx * 16, PL);
-#pragma unroll
-        for (int fc = 0; fc < FC; ++fc) {
-          const Frag<T> af = load_planes<T>(abase + (ck * 9 + tap) * 4 * UPL * WPL + fc * 256, WPL);
-#pragma unroll
-          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
-        }
-      }
-    }
-    if (rck) {  // ResnetBlock.res_conv 1x1 on the raw block input (fragments prefetched)
-#pragma unroll
-      for (int ck = 0; ck < RCKM; ++ck) {
-        if (ck >= rck) break;
-#pragma unroll
-        for (int fc = 0; fc < FC; ++fc) {
-          const Frag<T> af = load_planes<T>(rbase + ck * 4 * UPL * WPL + fc * 256, WPL);
-#pragma unroll
-          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, r2cur[ck][fp]);
-        }
-      }
-    }
-    // ---- epilogue: bias + embedding + residual, store, statistics ----
-#pragma unroll
-    for (int fp = 0; fp < FP; ++fp) {
-      const int po = (int)__umul24((y + prow[fp]) * W + pcol[fp], a.Cout);
-#pragma unroll
-      for (int fc = 0; fc < FC; ++fc) {
-        const int co = n0 + fc * 16 + 4 * g;
-        if (co >= a.Cout || (a.dbg & 16)) continue;
-        // statistics of the fp32 values (before the storage rounding), about the shift badd
-        float d[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) d[i] = acc[fp][fc][i];
-        if (a.res_mode == 1) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) d[i] += (float)r1cur[fp][fc][i];
-        }
-        store4<T>(outb + (po + co), d[0] + badd[fc][0], d[1] + badd[fc][1], d[2] + badd[fc][2], d[3] + badd[fc][3]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          s1[fc][i] += d[i];
-          s2[fc][i] += d[i] * d[i];
-        }
-      }
-    }
-    if (it + 1 < iters) commit_rows(fill, it + 1);
-    __syncthreads();
-  };
-  if (iters > 1) issue_rows(rowsB, 1);
-  if (iters > 2) issue_rows(rowsC, 2);
-  if (a.res_mode == 1) issue_res1(r1A, 0);
-  __syncthreads();                                         // initial ring rows visible
-  SDDM_STAMP(a, 3);
-  // rotation of the three row-group register sets: group j lives in set j % 3
-  for (int it = 0; it < iters; it += 6) {
-    body(it + 0, rowsA, rowsB, r1A, r1B);
-    if (it + 1 < iters) body(it + 1, rowsB, rowsC, r1B, r1A);
-    if (it + 2 < iters) body(it + 2, rowsC, rowsA, r1A, r1B);
-    if (it + 3 < iters) body(it + 3, rowsA, rowsB, r1B, r1A);
-    if (it + 4 < iters) body(it + 4, rowsB, rowsC, r1A, r1B);
-    if (it + 5 < iters) body(it + 5, rowsC, rowsA, r1B, r1A);
-  }
-
-  SDDM_STAMP(a, 4);
-  // ---- GroupNorm statistics of the strip: lanes -> waves -> block ----
-  // every lane of a channel sums about the same shift badd, so the sums add directly: the 16
-  // pixel lanes of a DPP row (VALU adds), then the waves through LDS
-  if (a.stats) {
-    const float nl = (float)(FP * iters) * 16.f;
-#pragma unroll
-    for (int fc = 0; fc < FC; ++fc)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float t1 = row_sum16(s1[fc][i]), t2 = row_sum16(s2[fc][i]);
-        if ((lane & 15) == 0) {
-          float* rr = red + ((wave * NBLK) + fc * 16 + 4 * g + i) * 3;
-          rr[0] = nl; rr[1] = t1; rr[2] = t2;
-        }
-      }
-    lds_sync();
-    if (tid < NBLK && n0 + tid < a.Cout) {
-      float n = 0.f, u1 = 0.f, u2 = 0.f;
-      for (int w = 0; w < NWV; ++w) {
-        const float* rr = red + (w * NBLK + tid) * 3;
-        n += rr[0]; u1 += rr[1]; u2 += rr[2];
-      }
-      const float shift = a.bias[n0 + tid] + (a.temb ? trow[n0 + tid] : 0.f);
-      float* dst = a.stats + (((size_t)b * a.n_tiles + strip) * a.Cout + n0 + tid) * 2;
-      dst[0] = (shift + u1 / n) * n;
-      dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);
-    }
-  }
-  SDDM_STAMP(a, 6);
-  SDDM_STAMP(a, 7);
-}
-
-template <typename T, int FC, int W, int CIN, int MPI>
-static size_t strip_lds(const ConvArgs& a) {
-  constexpr int ES = (int)sizeof(T), NBLK = 16 * FC, TR = MPI / W, R = 2 * TR + 2;
-  constexpr int UPP = CIN * ES / 16, PL = ((W + 2) * 16 + 255) / 256 * 256;
-  size_t n = (size_t)R * UPP * PL + (size_t)(CIN / 32) * 9 * 4 * (ES / 2) * NBLK * 16;
-  if (a.res_mode == 2) n += (size_t)((a.RCA + a.RCB) * ES / 16) * NBLK * 16;
-  n += (size_t)2 * CIN * 4 + (size_t)(MPI / 32) * NBLK * 3 * 4;
-  return n;
-}
-
-template <typename T, int FC, int W, int CIN, int MPI>
-static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size_t* lo) {
-  const size_t lds = strip_lds<T, FC, W, CIN, MPI>(a);
-  if (lo) { *lo = lds; return hipSuccess; }
-  constexpr int TR = MPI / W;
-  if (lds > 160 * 1024 || a.Ho % SR || SR % TR) return hipErrorInvalidValue;
-  const int nz = (a.Cout + 16 * FC - 1) / (16 * FC);
-  hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI>), dim3(a.Ho / SR, B, nz), dim3(MPI * 2), lds, s, a, SR);
-  return hipGetLastError();
-}
-
-// mpi: pixels per iteration (128 -> 4 waves, 256 -> 8 waves = two per SIMD)
 template <typename T>
-static hipError_t strip_dispatch(const ConvArgs& a, int nblk, int mpi, int SR, int B, hipStream_t s, size_t* lo) {
-  const int Cin = a.CA + a.CB;
-#define SDDM_STRIP(FCV, WV, CV)                                                                   \
-  if (nblk == 16 * FCV && a.Wo == WV && Cin == CV)                                                \
-    return mpi == 256 ? strip_go<T, FCV, WV, CV, 256>(a, SR, B, s, lo) : strip_go<T, FCV, WV, CV, 128>(a, SR, B, s, lo);
-  SDDM_STRIP(2, 128, 32) SDDM_STRIP(2, 128, 64) SDDM_STRIP(4, 128, 32) SDDM_STRIP(4, 128, 64)
-  SDDM_STRIP(2, 64, 32) SDDM_STRIP(2, 64, 64) SDDM_STRIP(2, 64, 128)
-  SDDM_STRIP(4, 64, 32) SDDM_STRIP(4, 64, 64) SDDM_STRIP(4, 64, 128)
-#undef SDDM_STRIP
-  if (lo) *lo = (size_t)1 << 40;
-  return hipErrorInvalidValue;
-}
+hipError_t strip_dispatch(const ConvArgs& a, int nblk, int mpi, int SR, int B, hipStream_t s, size_t* lo);
+extern template hipError_t strip_dispatch<bf16_t>(const ConvArgs&, int, int, int, int, hipStream_t, size_t*);
+extern template hipError_t strip_dispatch<f16_t>(const ConvArgs&, int, int, int, int, hipStream_t, size_t*);
+extern template hipError_t strip_dispatch<float>(const ConvArgs&, int, int, int, int, hipStream_t, size_t*);
 
 hipError_t launch_conv_strip(int dtype, int nblk, int mpi, int SR, const ConvArgs& a, int B, hipStream_t s) {
   if (dtype == DT_F32) return strip_dispatch<float>(a, nblk, mpi, SR, B, s, nullptr);

@@ -1,0 +1,414 @@
+// Row-streaming ("line buffer") 3x3 convolution (kernel template; instantiated per storage type
+// by conv_strip_bf16.hip / conv_strip_f16.hip / conv_strip_f32.hip, dispatched by conv_strip.hip) for the wide UNet levels (segment width W = 128
+// and 64: UNetModified2 levels 0-1, where >60 % of the FLOPs live).
+//
+// One block owns image b, output channels [n0, n0 + 16*FC) and a strip of SR output rows.  It
+// keeps in LDS
+//   * the weight slab of its channel tile (loaded once per strip, not once per tile), and
+//   * a ring of R = 2*TR + 2 transformed input rows (GroupNorm + SiLU applied once per element,
+//     zero halo columns, nearest-2x upsample / channel concat resolved while loading),
+// and walks the strip TR = MPI / W output rows at a time (MPI = 128 or 256 pixels, one wave per
+// 32 pixels = 2 MFMA column fragments; with MPI = 256 each SIMD runs two waves, so one wave's
+// GN+SiLU staging overlaps the other's MFMAs).  While the MFMAs of iteration i run on rows [y-1, y+TR] of the ring, each thread
+// already holds in registers the raw input of rows [y+TR+1, y+2TR] (issued before the MFMAs) and
+// writes them transformed into the free ring slots afterwards: one barrier per iteration.
+//
+// LDS images are plane-major (a plane = one 16-byte channel unit of every pixel / output channel,
+// plane stride = 0 mod 256 B): the 16 lanes of an MFMA operand read 16 consecutive 16-byte slots
+// and the ds_read_b128 lane groups never collide; staging writes go 8 consecutive pixels per
+// 8-lane group (conflict free) while the 64 lanes of a wave read 64/UPP whole pixels (coalesced).
+// Geometry (W, Cin) is compile-time so no integer division runs per element.
+// The epilogue adds bias, the noise-embedding projection and the residual (identity, or the
+// ResnetBlock 1x1 res_conv as extra MFMAs on raw input fragments loaded straight to registers),
+// stores 4 channels per lane, and accumulates GroupNorm statistics of the fp32 values in
+// registers (per-lane shifted sums, merged with Chan's formula at the end of the strip).
+//
+// Memory pipelining: the rows of row group j + 2 are issued at the top of iteration j into one of
+// two register sets (period-2 rotation, the loop unrolled by two) and committed at the end of
+// iteration j + 1, and the residual inputs (identity tile or res_conv fragments, RES = 1 / 2, a
+// template parameter so no load sits under a runtime branch) one iteration ahead.  Every body is
+// straight-line code, so the compiler's memory-counter waits are exact, and the iteration barrier
+// orders LDS only: no iteration waits for the loads it issued.
+#pragma once
+#include "conv_common.h"
+#include "kernels.h"
+
+namespace sddm {
+
+template <typename T, int FC, int W, int CIN, int MPI, int RES>
+__global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR) {
+  constexpr int NT = MPI * 2;                     // threads: one wave per 32 pixels of an iteration
+  constexpr int NWV = NT / 64;
+  constexpr int ES = (int)sizeof(T);
+  constexpr int NBLK = 16 * FC, FP = 2;
+  constexpr int TR = MPI / W, R = 2 * TR + 2;
+  constexpr int UPP = CIN * ES / 16;              // 16-byte channel units (planes) per pixel
+  constexpr int UPL = ES / 2;                     // units per lane group (8 channels)
+  constexpr int VE = 16 / ES;
+  constexpr int PL = ((W + 2) * 16 + 255) / 256 * 256;
+  constexpr int SLOT = UPP * PL;
+  constexpr int NCK = CIN / 32;
+  constexpr int WPL = NBLK * 16;                  // weight plane stride
+  constexpr int WPLANES = NCK * 9 * 4 * UPL;
+  constexpr int PB = 64 / UPP;                    // pixels per 64-unit staging group
+  constexpr int NU = TR * W * UPP;                // units of TR rows
+  constexpr int UPT = NU / NT;                    // prefetch units per thread and row group
+  constexpr int IU = ((TR + 2) * W * UPP + NT - 1) / NT;   // initial-row units per thread
+  constexpr int RCKM = 4;                         // res_conv chunks held in registers (RC <= 128)
+  static_assert(UPP >= 1 && UPP <= 64 && (64 % UPP) == 0, "channel units must divide a wave");
+  static_assert(NU % NT == 0, "prefetch must split evenly");
+  typedef T vec4 __attribute__((ext_vector_type(4)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int strip = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NBLK;
+  const int H = a.Ho;
+  const int RC = a.RCA + a.RCB;
+  const int rck = RES == 2 ? RC / 32 : 0;
+  const bool gn = a.gamma != nullptr;
+
+  char* ring = smem;                              // [R][UPP planes][PL]
+  char* wl = ring + R * SLOT;                     // [WPLANES][NBLK][16 B]
+  char* rw = wl + WPLANES * WPL;                  // [RC*ES/16 planes][NBLK][16 B]
+  const int RPLANES = rck * 32 * ES / 16;
+  float* gsc = (float*)(rw + RPLANES * WPL);      // [2][CIN]
+  float* red = gsc + 2 * CIN;                     // [NWV waves][NBLK][3]
+
+  const int y0 = strip * SR;
+  const int iters = SR / TR;                      // even (checked by the launcher)
+  SDDM_STAMP(a, 0);
+  // ---------------- prologue: every independent load issued before anything waits ----------------
+  GNLoad gl;
+  const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
+  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
+  // initial ring rows y0-1 .. y0+TR (raw), clamped addresses, zero rows outside the image later
+  const T* srcAb = (const T*)a.srcA + (size_t)b * a.Hi * a.Wi * a.CA;
+  const T* srcBb = a.CB ? (const T*)a.srcB + (size_t)b * a.Hi * a.Wi * a.CB : srcAb;
+  f32x4 ini[IU];
+#pragma unroll
+  for (int k = 0; k < IU; ++k) {
+    const int u = min(tid + k * NT, (TR + 2) * W * UPP - 1);
+    const int grp = u >> 6, j = u & 63;
+    const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
+    const int ry = min(max(y0 - 1 + r, 0), H - 1);
+    const int sy = a.upsample ? ry >> 1 : ry, sx = a.upsample ? x >> 1 : x;
+    const int c0 = q * VE;
+    const bool fa = c0 < a.CA;
+    ini[k] = *(const f32x4*)((fa ? srcAb : srcBb) + ((size_t)sy * a.Wi + sx) * (fa ? a.CA : a.CB) + (fa ? c0 : c0 - a.CA));
+  }
+  // weight slabs straight into LDS (LDS-DMA: unit u lands at byte 16 u, co fastest, so every
+  // wave-instruction fills 1 KiB of consecutive LDS; no VGPRs, no wait until the first barrier)
+  // NBLK * WPLANES and NBLK * RPLANES are multiples of 64: whole waves, no tail
+  for (int u0 = wave * 64; u0 < NBLK * WPLANES; u0 += NT) {
+    const int u = u0 + lane;
+    const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
+    const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
+    const char* src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(wl + u0 * 16), 16, 0, 0);
+  }
+  if constexpr (RES == 2) {
+    for (int u0 = wave * 64; u0 < NBLK * RPLANES; u0 += NT) {
+      const int u = u0 + lane;
+      const int co = u % NBLK, pl = u / NBLK;
+      const char* src = (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                       (__attribute__((address_space(3))) void*)(rw + u0 * 16), 16, 0, 0);
+    }
+  }
+  for (int u = tid; u < R * UPP * 2; u += NT) {           // zero halo columns
+    const int side = u & 1, pl = u >> 1;
+    *(f32x4*)(ring + pl * PL + (side ? (W + 1) : 0) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + CIN);
+  __syncthreads();                                         // gsc ready
+  // bias + noise embedding of this lane's epilogue channels (Cout % NBLK == 0: no clamping)
+  const int t_now = a.t_dev ? *a.t_dev : 0;
+  const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
+  float badd[FC][4];
+#pragma unroll
+  for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int co = n0 + fc * 16 + 4 * g + i;
+      const float bv = a.bias[co], tv = trow[co];
+      badd[fc][i] = bv + (a.temb ? tv : 0.f);
+    }
+  // the statistics shift of channel n0 + tid (threads tid < NBLK write the tile statistics):
+  // loaded here so the end of the strip does not wait a memory round trip for it
+  float sshift;
+  {
+    const int cs = n0 + (tid % NBLK);
+    const float bv = a.bias[cs], tv = trow[cs];
+    sshift = bv + (a.temb ? tv : 0.f);
+  }
+  const int base = ((y0 - 1) % R + R) % R;                 // ring slot of row y0 - 1
+#pragma unroll
+  for (int k = 0; k < IU; ++k) {
+    const int u = tid + k * NT;
+    if (u >= (TR + 2) * W * UPP) break;
+    const int grp = u >> 6, j = u & 63;
+    const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
+    const int ry = y0 - 1 + r;
+    f32x4 v = ini[k];
+    if (ry < 0 || ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
+    else if (gn) v = transform_fast<T>(v, gsc + q * VE, gsc + CIN + q * VE);
+    *(f32x4*)(ring + ((base + r) % R) * SLOT + q * PL + (x + 1) * 16) = v;
+  }
+
+  int prow[FP], pcol[FP];
+#pragma unroll
+  for (int fp = 0; fp < FP; ++fp) {
+    const int p = wave * 32 + fp * 16 + (lane & 15);   // pixel inside the MPI-pixel iteration
+    prow[fp] = p / W;
+    pcol[fp] = p % W;
+  }
+  // row-group prefetch geometry of this thread's units (the same every iteration)
+  // (all per-iteration address math below is 32-bit with 24-bit multiplies: full-rate VALU)
+  int pr[UPT], uoff[UPT], loff[UPT], cq[UPT];  // row in group, source offset (elements, +A/B flag), LDS offset, channel
+#pragma unroll
+  for (int k = 0; k < UPT; ++k) {
+    const int u = tid + k * NT, grp = u >> 6, j = u & 63;
+    const int pix = grp * PB + (j % PB);
+    const int q = j / PB, x = pix % W;
+    pr[k] = pix / W;
+    loff[k] = q * PL + (x + 1) * 16;
+    cq[k] = q * VE;
+    const int c0 = q * VE;
+    const int sx = a.upsample ? (x >> 1) : x;
+    const bool fa = c0 < a.CA;
+    uoff[k] = (fa ? sx * a.CA + c0 : sx * a.CB + (c0 - a.CA)) * 2 + (fa ? 0 : 1);
+  }
+  const int rsA = a.Wi * a.CA, rsB = a.Wi * a.CB;          // elements per source row
+  // rows of row group j (clamped: the groups past the strip end load valid rows nobody reads)
+  auto issue_rows = [&](f32x4 (&dst)[UPT], int j) {
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int ry = min(y0 + j * TR + 1 + pr[k], H - 1);
+      const int sy = a.upsample ? (ry >> 1) : ry;
+      const bool fb = uoff[k] & 1;
+      dst[k] = *(const f32x4*)((fb ? srcBb : srcAb) + ((uoff[k] >> 1) + (int)__umul24(sy, fb ? rsB : rsA)));
+    }
+  };
+  // ring slots of row group j (group iters, past the strip, lands in slots nobody reads again)
+  auto commit_rows = [&](const f32x4 (&src)[UPT], int j) {
+    const int sb = (base + j * TR + 2) % R;             // uniform
+#pragma unroll
+    for (int k = 0; k < UPT; ++k) {
+      const int ry = y0 + j * TR + 1 + pr[k];
+      f32x4 v = src[k];
+      if (ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
+      else if (gn) v = transform_lds<T>(v, gsc + cq[k], gsc + CIN + cq[k]);
+      int sl = sb + pr[k];
+      sl = sl >= R ? sl - R : sl;
+      *(f32x4*)(ring + (int)__umul24(sl, SLOT) + loff[k]) = v;
+    }
+  };
+  T* outb = (T*)a.out + (size_t)b * H * W * a.Cout;
+  // residual inputs of iteration it (issued one iteration ahead; rows clamped into the image)
+  const T* resb = RES == 1 ? (const T*)a.res_src + (size_t)b * H * W * a.Cout : outb;
+  auto issue_res1 = [&](vec4 (&dst)[FP][FC], int it) {
+#pragma unroll
+    for (int fp = 0; fp < FP; ++fp) {
+      const int yy = min(y0 + it * TR, H - TR) + prow[fp];
+      const int po = (int)__umul24(yy * W + pcol[fp], a.Cout);
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) dst[fp][fc] = *(const vec4*)(resb + (po + n0 + fc * 16 + 4 * g));
+    }
+  };
+  const T* rawAb = RES == 2 ? (const T*)a.rawA + (size_t)b * H * W * a.RCA : outb;
+  const T* rawBb = (RES == 2 && a.RCB) ? (const T*)a.rawB + (size_t)b * H * W * a.RCB : rawAb;
+  auto issue_res2 = [&](Frag<T> (&dst)[RCKM][FP], int it) {
+#pragma unroll
+    for (int ck = 0; ck < RCKM; ++ck)
+#pragma unroll
+      for (int fp = 0; fp < FP; ++fp) {
+        const int yy = min(y0 + it * TR, H - TR) + prow[fp];
+        const int c0 = min(ck, rck - 1) * 32 + g * 8;
+        const int pix = yy * W + pcol[fp];
+        const T* sp = c0 < a.RCA ? rawAb + ((int)__umul24(pix, a.RCA) + c0) : rawBb + ((int)__umul24(pix, a.RCB) + (c0 - a.RCA));
+        dst[ck][fp] = load_frag<T>((const char*)sp);
+      }
+  };
+
+  // per-lane sums of (value - badd) (shift = bias + embedding) as packed pairs matching the
+  // accumulator register pairs: the epilogue is v_pk_add / v_pk_fma, no shuffles
+  f32x2 s1[FC][2], s2[FC][2], bp[FC][2];
+#pragma unroll
+  for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      s1[fc][h] = f32x2{0.f, 0.f};
+      s2[fc][h] = f32x2{0.f, 0.f};
+      bp[fc][h] = f32x2{badd[fc][2 * h], badd[fc][2 * h + 1]};
+    }
+  const char* abase = wl + g * UPL * WPL + (lane & 15) * 16;
+  const char* rbase = rw + g * UPL * WPL + (lane & 15) * 16;
+
+  // one iteration: loads of row group it+2 and the next residual inputs, MFMAs on the ring rows
+  // of row group it, epilogue, ring refill with row group it+1 (issued one iteration earlier)
+  f32x4 rowsA[UPT], rowsB[UPT];
+  vec4 r1A[FP][FC], r1B[FP][FC];
+  Frag<T> r2A[RCKM][FP], r2B[RCKM][FP];
+  auto body = [&](int it, f32x4 (&nxt)[UPT], f32x4 (&fill)[UPT], vec4 (&r1cur)[FP][FC], vec4 (&r1nxt)[FP][FC],
+                  Frag<T> (&r2cur)[RCKM][FP], Frag<T> (&r2nxt)[RCKM][FP]) {
+    const int y = y0 + it * TR;
+    const int s_it = (base + it * TR) % R;               // slot of row y - 1
+    issue_rows(nxt, it + 2);
+    if constexpr (RES == 1) issue_res1(r1nxt, it + 1);
+    if constexpr (RES == 2) issue_res2(r2nxt, it + 1);
+    // keep these loads at the top of the body: the scheduler would otherwise sink them below the
+    // MFMAs (shorter live ranges) and halve the prefetch distance
+    __builtin_amdgcn_sched_barrier(0);
+    f32x4 acc[FP][FC];
+#pragma unroll
+    for (int i = 0; i < FP; ++i)
+#pragma unroll
+      for (int j = 0; j < FC; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* bptr[FP][3];
+#pragma unroll
+    for (int fp = 0; fp < FP; ++fp)
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) {
+        int sl = s_it + prow[fp] + dy;                   // < 2R: one conditional wrap
+        sl = sl >= R ? sl - R : sl;
+        bptr[fp][dy] = ring + (int)__umul24(sl, SLOT) + g * UPL * PL + pcol[fp] * 16;
+      }
+#pragma unroll
+    for (int ck = 0; ck < NCK; ++ck) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int dy = tap / 3, dx = tap - 3 * dy;
+        Frag<T> bf[FP];
+#pragma unroll
+        for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(bptr[fp][dy] + ck * 4 * UPL * PL + dx * 16, PL);
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) {
+          const Frag<T> af = load_planes<T>(abase + (ck * 9 + tap) * 4 * UPL * WPL + fc * 256, WPL);
+#pragma unroll
+          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
+        }
+      }
+    }
+    if constexpr (RES == 2) {  // ResnetBlock.res_conv 1x1 on the raw block input (fragments prefetched)
+#pragma unroll
+      for (int ck = 0; ck < RCKM; ++ck) {
+        if (ck >= rck) break;
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) {
+          const Frag<T> af = load_planes<T>(rbase + ck * 4 * UPL * WPL + fc * 256, WPL);
+#pragma unroll
+          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, r2cur[ck][fp]);
+        }
+      }
+    }
+    // ---- epilogue: bias + embedding + residual, store, statistics ----
+#pragma unroll
+    for (int fp = 0; fp < FP; ++fp) {
+      const int po = (int)__umul24((y + prow[fp]) * W + pcol[fp], a.Cout);
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) {
+        const int co = n0 + fc * 16 + 4 * g;
+        // statistics of the fp32 values (before the storage rounding), about the shift badd
+        f32x2 d0 = f32x2{acc[fp][fc][0], acc[fp][fc][1]}, d1 = f32x2{acc[fp][fc][2], acc[fp][fc][3]};
+        if constexpr (RES == 1) {
+          d0 += unpack2<T>(r1cur[fp][fc][0], r1cur[fp][fc][1]);
+          d1 += unpack2<T>(r1cur[fp][fc][2], r1cur[fp][fc][3]);
+        }
+        store4p<T>(outb + (po + co), d0 + bp[fc][0], d1 + bp[fc][1]);
+        s1[fc][0] += d0;
+        s1[fc][1] += d1;
+        s2[fc][0] = __builtin_elementwise_fma(d0, d0, s2[fc][0]);
+        s2[fc][1] = __builtin_elementwise_fma(d1, d1, s2[fc][1]);
+      }
+    }
+    commit_rows(fill, it + 1);
+    lds_sync();                                          // LDS only: the prefetches stay in flight
+  };
+  issue_rows(rowsA, 1);
+  if constexpr (RES == 1) issue_res1(r1A, 0);
+  if constexpr (RES == 2) issue_res2(r2A, 0);
+  // the weight DMA and the initial ring must have landed before the first MFMA; the NYOUNG loads
+  // just issued stay in flight (a counted wait: everything older has completed)
+  constexpr int NYOUNG = UPT + (RES == 1 ? FP * FC : 0) + (RES == 2 ? RCKM * FP : 0);
+  static_assert(NYOUNG < 64, "vmcnt is a 6-bit counter");
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(NYOUNG) : "memory");
+  SDDM_STAMP(a, 3);
+  for (int it = 0; it < iters; it += 2) {                // period-2 rotation of the register sets
+    body(it, rowsB, rowsA, r1A, r1B, r2A, r2B);
+    body(it + 1, rowsA, rowsB, r1B, r1A, r2B, r2A);
+  }
+
+  SDDM_STAMP(a, 4);
+  // ---- GroupNorm statistics of the strip: lanes -> waves -> block ----
+  // every lane of a channel sums about the same shift badd, so the sums add directly: the 16
+  // pixel lanes of a DPP row (VALU adds), then the waves through LDS
+  if (a.stats) {
+    const float nl = (float)(FP * iters) * 16.f;
+#pragma unroll
+    for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float t1 = row_sum16(s1[fc][i >> 1][i & 1]), t2 = row_sum16(s2[fc][i >> 1][i & 1]);
+        if ((lane & 15) == 0) {
+          float* rr = red + ((wave * NBLK) + fc * 16 + 4 * g + i) * 3;
+          rr[0] = nl; rr[1] = t1; rr[2] = t2;
+        }
+      }
+    lds_sync();
+    if (tid < NBLK) {
+      float n = 0.f, u1 = 0.f, u2 = 0.f;
+      for (int w = 0; w < NWV; ++w) {
+        const float* rr = red + (w * NBLK + tid) * 3;
+        n += rr[0]; u1 += rr[1]; u2 += rr[2];
+      }
+      float* dst = a.stats + (((size_t)b * a.n_tiles + strip) * a.Cout + n0 + tid) * 2;
+      dst[0] = (sshift + u1 / n) * n;
+      dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);
+    }
+  }
+  SDDM_STAMP(a, 6);
+  SDDM_STAMP(a, 7);
+}
+
+template <typename T, int FC, int W, int CIN, int MPI>
+static size_t strip_lds(const ConvArgs& a) {
+  constexpr int ES = (int)sizeof(T), NBLK = 16 * FC, TR = MPI / W, R = 2 * TR + 2;
+  constexpr int UPP = CIN * ES / 16, PL = ((W + 2) * 16 + 255) / 256 * 256;
+  size_t n = (size_t)R * UPP * PL + (size_t)(CIN / 32) * 9 * 4 * (ES / 2) * NBLK * 16;
+  if (a.res_mode == 2) n += (size_t)((a.RCA + a.RCB) * ES / 16) * NBLK * 16;
+  n += (size_t)2 * CIN * 4 + (size_t)(MPI / 32) * NBLK * 3 * 4;
+  return n;
+}
+
+template <typename T, int FC, int W, int CIN, int MPI>
+static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size_t* lo) {
+  const size_t lds = strip_lds<T, FC, W, CIN, MPI>(a);
+  if (lo) { *lo = lds; return hipSuccess; }
+  constexpr int TR = MPI / W;
+  if (lds > 160 * 1024 || a.Ho % SR || SR % (2 * TR) || a.Cout % (16 * FC) || a.res_mode < 0 || a.res_mode > 2 ||
+      (a.res_mode == 2 && (a.RCA + a.RCB) > 128))
+    return hipErrorInvalidValue;
+  const dim3 grid(a.Ho / SR, B, a.Cout / (16 * FC)), blk(MPI * 2);
+  if (a.res_mode == 0) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0>), grid, blk, lds, s, a, SR);
+  else if (a.res_mode == 1) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 1>), grid, blk, lds, s, a, SR);
+  else hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 2>), grid, blk, lds, s, a, SR);
+  return hipGetLastError();
+}
+
+// mpi: pixels per iteration (128 -> 4 waves, 256 -> 8 waves = two per SIMD)
+template <typename T>
+hipError_t strip_dispatch(const ConvArgs& a, int nblk, int mpi, int SR, int B, hipStream_t s, size_t* lo) {
+  const int Cin = a.CA + a.CB;
+#define SDDM_STRIP(FCV, WV, CV)                                                                   \
+  if (nblk == 16 * FCV && a.Wo == WV && Cin == CV)                                                \
+    return mpi == 256 ? strip_go<T, FCV, WV, CV, 256>(a, SR, B, s, lo) : strip_go<T, FCV, WV, CV, 128>(a, SR, B, s, lo);
+  SDDM_STRIP(2, 128, 32) SDDM_STRIP(2, 128, 64) SDDM_STRIP(4, 128, 32) SDDM_STRIP(4, 128, 64)
+  SDDM_STRIP(2, 64, 32) SDDM_STRIP(2, 64, 64) SDDM_STRIP(2, 64, 128)
+  SDDM_STRIP(4, 64, 32) SDDM_STRIP(4, 64, 64) SDDM_STRIP(4, 64, 128)
+#undef SDDM_STRIP
+  if (lo) *lo = (size_t)1 << 40;
+  return hipErrorInvalidValue;
+}
+
+}  // namespace sddm

@@ -125,6 +125,12 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
       const float bv = a.bias[co], tv = trow[co];
       bb[fc][i] = bv + (a.temb ? tv : 0.f);
     }
+  float sshift;                                            // statistics shift of channel n0 + tid (tid < NB)
+  {
+    const int cs = n0 + (tid % NB);
+    const float bv = a.bias[cs], tv = trow[cs];
+    sshift = bv + (a.temb ? tv : 0.f);
+  }
   // this lane's output pixels (MFMA column c16 of each pixel fragment)
   int ppy[FP], ppx[FP];
   bool pok[FP];
@@ -352,9 +358,8 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
         const float* e = red + (w * NB + tid) * 3;
         n += e[0]; t1 += e[1]; t2 += e[2];
       }
-      const int co = tid;                                   // bb of this channel: lane (co % 16) / 4 ...
-      const float shift = a.bias[n0 + co] + (a.temb ? trow[n0 + co] : 0.f);
-      const float mean = shift + t1 / n;
+      const int co = tid;
+      const float mean = sshift + t1 / n;
       float* dst = a.stats + (((size_t)b * a.n_tiles + tile) * a.Cout + n0 + co) * 2;
       dst[0] = mean * n;
       dst[1] = fmaxf(t2 - t1 * t1 / n, 0.f);

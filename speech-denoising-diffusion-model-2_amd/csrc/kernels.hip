@@ -147,15 +147,27 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   if (a.t_dev && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.t_dev -= 1;
   SDDM_STAMP(a, 0);
   const int S = a.S, F = a.F, W = a.W, IW = W + 2, IH = a.TR + 2;
-  {
+  {  // every load of the frame image issued before the first is stored (clamped addresses:
+     // a load under a condition is waited for at the branch join)
     const float* c0 = a.cond + (size_t)b * a.N;
     const float* x0 = a.x + (size_t)b * a.N;
-    for (int i = tid; i < IH * IW; i += 256) {
+    constexpr int IPT = (IMAX + 255) / 256;
+    float cv[IPT], xv[IPT];
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = min(tid + 256 * k, IH * IW - 1);
       const int r = i / IW, c = i - r * IW, f = f0 - 1 + r, w = c - 1;
       const bool ok = f >= 0 && f < F && w >= 0 && w < W;
       const int n = ok ? f * S + w : 0;
-      img[0][i] = ok ? c0[n] : 0.f;
-      img[1][i] = ok ? x0[n] : 0.f;
+      cv[k] = c0[n];
+      xv[k] = x0[n];
+      cv[k] = ok ? cv[k] : 0.f;
+      xv[k] = ok ? xv[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < IPT; ++k) {
+      const int i = tid + 256 * k;
+      if (i < IH * IW) { img[0][i] = cv[k]; img[1][i] = xv[k]; }
     }
   }
   float bias[2][4];
@@ -252,17 +264,14 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   for (int fc = 0; fc < 2; ++fc)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {
-        st1[fc][i] += __shfl_xor(st1[fc][i], o);
-        st2[fc][i] += __shfl_xor(st2[fc][i], o);
-      }
+      st1[fc][i] = row_sum16(st1[fc][i]);                   // DPP row adds (VALU)
+      st2[fc][i] = row_sum16(st2[fc][i]);
       if ((lane & 15) == 0) {
         xs_red[wave][fc * 16 + 4 * g + i][0] = st1[fc][i];
         xs_red[wave][fc * 16 + 4 * g + i][1] = st2[fc][i];
       }
     }
-  __syncthreads();
+  lds_sync();                                              // (the output stores stay in flight)
   SDDM_STAMP(a, 3);
   if (tid < CO) {
     const float n = (float)(a.TR * W);
@@ -365,20 +374,49 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
   float* y = P + 9 * PR * PC;                 // [YR][W]
   float* gs = y + YR * W;                     // [2][C]
   SDDM_STAMP(a, 0);
-  {
-    const GNFuse gf{a.gst, a.gtiles, a.gntile, nullptr, 0, 0, a.gamma, a.beta, a.groups, a.eps};
-    GNLoad gl;
-    gl.issue(gf, b, C, 0, true, a.gamma);
-    gl.finish(gf, b, C, 0, gs, gs + C);
-  }
-  __syncthreads();
-  SDDM_STAMP(a, 1);
+  // every independent load first: the transition's x_t / condition (one 4-sample vector per
+  // thread: the block's samples fit one pass, checked by the launcher), the GroupNorm statistics
+  // and the first pass of activation fragments; then one wait
+  const int n_begin = f0 * S;
+  const int n_end = (f0 + a.FT >= F) ? a.N : (f0 + a.FT) * S;
+  float* xrow = a.x + (size_t)b * a.N;
+  const float* crow = a.cond ? a.cond + (size_t)b * a.N : xrow;
+  const int n4 = n_begin + 4 * tid;
+  const int n4c = n4 < n_end ? n4 : n_begin;
+  const f32x4 xin = *(const f32x4*)(xrow + n4c);
+  const f32x4 cin = *(const f32x4*)(crow + n4c);
+  const GNFuse gf{a.gst, a.gtiles, a.gntile, nullptr, 0, 0, a.gamma, a.beta, a.groups, a.eps};
+  GNLoad gl;
+  gl.issue(gf, b, C, 0, true, a.gamma);
   // phase 1 as an MFMA: P[tap][pos] = sum_c w[c][tap] * silu(gn(x[c][pos])) with A = the 9 taps
   // (rows, padded to 16) x 32 channels and B = 32 channels x 16 positions.  bf16 / f16: fp16
   // hi/lo split of both operands (fp32-accurate products); float: exact f32 MFMA.
   const int lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const T* src = (const T*)a.src + (size_t)b * F * W * C;
   const int tapr = lane & 15;
+  const int npos = PR * PC, nfr = (npos + 15) / 16;
+  // every fragment of this wave is loaded before the first is used (one memory latency, not one
+  // per fragment): FRW fragments per pass
+  constexpr int NWV = 8, FRW = 12;                   // waves per block, fragments per wave and pass
+  constexpr int NV = (int)sizeof(T) * 8 / 16;        // 16-byte vectors per 8 channels
+  typedef T vec8 __attribute__((ext_vector_type(8)));
+  f32x4 xr[FRW][NV];
+  auto load_pass = [&](int fr0) {
+#pragma unroll
+    for (int q = 0; q < FRW; ++q) {
+      const int pp = (fr0 + NWV * q) * 16 + (lane & 15);
+      const int r = pp / PC, col = pp - r * PC;
+      const int f = f0 - back - 1 + r, w = col - 1;
+      const bool in = pp < npos && f >= 0 && f < F && w >= 0 && w < W;
+      const size_t off = in ? ((size_t)f * W + w) * C + 8 * g : 8 * g;
+#pragma unroll
+      for (int h = 0; h < NV; ++h) xr[q][h] = *(const f32x4*)((const char*)(src + off) + 16 * h);
+    }
+  };
+  load_pass(wave);
+  gl.finish(gf, b, C, 0, gs, gs + C);
+  lds_sync();                                        // scale / shift visible (loads stay in flight)
+  SDDM_STAMP(a, 1);
   float wv[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
@@ -387,24 +425,8 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
     sc[j] = gs[c];
     sh[j] = gs[C + c];
   }
-  const int npos = PR * PC, nfr = (npos + 15) / 16;
-  // every fragment of this wave is loaded before the first is used (one memory latency, not one
-  // per fragment): FRW fragments per pass
-  constexpr int NWV = 8, FRW = 12;                   // waves per block, fragments per wave and pass
-  typedef T vec8 __attribute__((ext_vector_type(8)));
   for (int fr0 = wave; fr0 < nfr; fr0 += NWV * FRW) {
-  constexpr int NV = (int)sizeof(T) * 8 / 16;        // 16-byte vectors per 8 channels
-  f32x4 xr[FRW][NV];
-#pragma unroll
-  for (int q = 0; q < FRW; ++q) {
-    const int pp = (fr0 + NWV * q) * 16 + (lane & 15);
-    const int r = pp / PC, col = pp - r * PC;
-    const int f = f0 - back - 1 + r, w = col - 1;
-    const bool in = pp < npos && f >= 0 && f < F && w >= 0 && w < W;
-    const size_t off = in ? ((size_t)f * W + w) * C + 8 * g : 8 * g;
-#pragma unroll
-    for (int h = 0; h < NV; ++h) xr[q][h] = *(const f32x4*)((const char*)(src + off) + 16 * h);
-  }
+  if (fr0 != wave) load_pass(fr0);                   // inputs larger than one pass
 #pragma unroll
   for (int q = 0; q < FRW; ++q) {
     const int fr = fr0 + NWV * q;
@@ -445,7 +467,7 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
         if (4 * g + i < 9) P[((4 * g + i) * PR + r) * PC + col] = acc[i];
   }
   }
-  __syncthreads();
+  lds_sync();
   SDDM_STAMP(a, 2);
   for (int p = tid; p < YR * W; p += blockDim.x) {
     const int r = p / W, w = p - r * W;        // y row r <-> P rows r .. r+2, cols w .. w+2
@@ -456,17 +478,13 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
       for (int dx = 0; dx < 3; ++dx) s += P[((dy * 3 + dx) * PR + r + dy) * PC + w + dx];
     y[p] = s + a.bias;
   }
-  __syncthreads();
+  lds_sync();
   SDDM_STAMP(a, 3);
-  const int n_begin = f0 * S;
-  const int n_end = (f0 + a.FT >= F) ? a.N : (f0 + a.FT) * S;
   const int t = a.t_dev ? *a.t_dev : 0;
-  float* xrow = a.x + (size_t)b * a.N;
-  const float* crow = a.cond ? a.cond + (size_t)b * a.N : nullptr;
   const uint64_t seed = a.sp ? a.sp->seed : a.seed;
   const int64_t row_offset = a.sp ? a.sp->row_offset : a.row_offset;
   const int64_t ebase = (row_offset + b) * (int64_t)a.N;
-  for (int n4 = n_begin + 4 * tid; n4 < n_end; n4 += 4 * blockDim.x) {
+  if (n4 < n_end) {
     const uint64_t e0 = (uint64_t)(ebase + n4);
     f32x4 z = {0.f, 0.f, 0.f, 0.f};
     const bool aligned = (e0 & 3) == 0;
@@ -484,7 +502,7 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
         a.eps_out[(size_t)b * a.N + n] = e;
       } else {
         const float zz = (t > 1) ? (aligned ? z[j] : philox_normal1(seed, (uint32_t)t, e0 + j)) : 0.f;
-        xrow[n] = transition_one(a.mode, a.co, t, xrow[n], e, crow ? crow[n] : 0.f, zz);
+        xrow[n] = transition_one(a.mode, a.co, t, xin[j], e, a.cond ? cin[j] : 0.f, zz);
       }
     }
   }
@@ -495,7 +513,8 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
   const int back = a.W / a.S - 1, YR = a.FT + back;
   const size_t lds = ((size_t)9 * (YR + 2) * (a.W + 2) + (size_t)YR * a.W + 2 * a.C) * 4;
-  if (lds > 160 * 1024 || a.F % a.FT || a.C != 32) return hipErrorInvalidValue;
+  // one pass of 4 samples per thread covers a block's samples (the last block's tail included)
+  if (lds > 160 * 1024 || a.F % a.FT || a.C != 32 || a.FT * a.S + a.W > 4 * 512 || a.N % 4) return hipErrorInvalidValue;
   dim3 grid(a.F / a.FT, B);
   if (dtype == DT_F32) hipLaunchKernelGGL(final_kernel<float>, grid, dim3(512), lds, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(final_kernel<bf16_t>, grid, dim3(512), lds, s, a);

@@ -64,8 +64,13 @@ def main():
         nz = [k for k in range(1, 7) if st[:, k].any()]
         ph = [f"{k0}->{k1}: {np.mean(st[:, k1] - st[:, k0]):8.0f}" for k0, k1 in zip(nz[:-1], nz[1:])]
         cyc = st[:, 6] - st[:, 1] if st[:, 1].any() else st[:, 6] - st[:, 3]
+        ev = sorted([(x, 1) for x in t0] + [(x, -1) for x in t7], key=lambda e: (e[0], e[1]))
+        cur = conc = 0
+        for _, d in ev:
+            cur += d
+            conc = max(conc, cur)
         print(f"{op}: {n.value} blocks, span {span:.1f} us, block dur mean {dur.mean():.2f} max {dur.max():.2f} us, "
-              f"start spread max {start.max():.2f} us (p50 {np.median(start):.2f})")
+              f"start spread max {start.max():.2f} us (p50 {np.median(start):.2f}), max concurrent blocks {conc}")
         print("   cycles " + "  ".join(ph) + f"   (sum {cyc.mean():.0f} cyc)")
         ctx.close()
 
