@@ -45,16 +45,16 @@ __host__ __device__ inline DeepGeo deep_geo(bool s2, int TR, int TW, int MT) {
 // LDS byte layout of one block; region 0 (the staged image) is reused for the partial tiles
 struct DeepLds { int rres, badd, gsc, total; };
 
-template <typename T, int MT, int NW>
+template <typename T, int MT, int NW, int NB>
 __host__ __device__ inline DeepLds deep_layout(const DeepGeo& g, int nck, int rck, int Cin, bool ident) {
-  constexpr int ES = (int)sizeof(T), UPP = 2 * ES, NBP = 36;
+  constexpr int ES = (int)sizeof(T), UPP = 2 * ES, NBP = NB + 4;
   constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;   // two-stage reduction for 8 x 128 pixels
   const int red = SLOTS * MT * NBP * 4;
   const int stage = nck * UPP * g.PLB + rck * UPP * g.PLR;
   DeepLds L;
   int off = stage > red ? stage : red;
   L.rres = off;
-  off += ident ? MT * 32 * ES : 0;
+  off += ident ? MT * NB * ES : 0;
   L.badd = off;
   off += 32 * 4;
   L.gsc = off;
@@ -74,14 +74,17 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   n = nt;
 }
 
-template <typename T, bool S2, int MT, int NW, int D>
+template <typename T, bool S2, int MT, int NW, int D, int NB>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) {
   constexpr int NT = 64 * NW;
   constexpr int ES = (int)sizeof(T);
   constexpr int UPP = 2 * ES;          // 16-byte planes per 32-channel chunk
   constexpr int UPL = ES / 2;          // planes per MFMA lane group (8 channels)
   constexpr int VE = 16 / ES;          // channels per plane
-  constexpr int FP = MT / 16, FC = 2, NB = 32, NBP = NB + 4;
+  constexpr int FP = MT / 16, FC = NB / 16, NBP = NB + 4;
+  constexpr int TPP = NB / 4;          // epilogue threads per pixel (4 channels each)
+  constexpr int UPR = NB * ES / 16;    // 16-byte units of one pixel's identity-residual channels
+  static_assert(NB == 16 || NB == 32, "16 or 32 output channels per block");
   constexpr int MAXU = ES == 4 ? (NW == 8 ? 6 : 8) : (NW == 8 ? 10 : 16);   // units per thread per pass
   constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -97,7 +100,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   const int Cin = a.CA + a.CB, nck = Cin / 32;
   const int RC = a.RCA + a.RCB, rck = a.res_mode == 2 ? RC / 32 : 0;
   const bool gn = a.gamma != nullptr, ident = a.res_mode == 1;
-  const DeepLds lay = deep_layout<T, MT, NW>(geo, nck, rck, Cin, ident);
+  const DeepLds lay = deep_layout<T, MT, NW, NB>(geo, nck, rck, Cin, ident);
   float* gsc = (float*)(smem + lay.gsc);                 // [2][Cin] GroupNorm scale / shift
   const int res_off = nck * UPP * PLB;
   const int img_in = a.Hi * a.Wi, img_out = a.Ho * a.Wo;
@@ -119,7 +122,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   const int n3 = (HP + 7) / 8 * 8 * nq3;
   const int nqr = rck * UPP;
   const int nres = nqr * MT;
-  const int total = n3 + nres + (ident ? MT * UPP : 0);
+  const int total = n3 + nres + (ident ? MT * UPR : 0);
   const float rnq3 = 1.0f / (float)max(nq3, 1), rnqr = 1.0f / (float)max(nqr, 1);
   const float rHC = 1.0f / (float)HC, rTW = 1.0f / (float)a.TW;
   // packed destination: LDS byte offset << 10 | (GroupNorm channel + 2); -2 = zero, -1 = raw copy
@@ -155,8 +158,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
               (fromA ? c : c - a.RCA);
         gs = -1;
       }
-    } else if (u < total) {            // identity residual [p][32 channels]
-      const int v = u - n3 - nres, p = v / UPP, q = v - p * UPP;
+    } else if (u < total) {            // identity residual [p][NB channels]
+      const int v = u - n3 - nres, p = v / UPR, q = v - p * UPR;
       d = lay.rres + v * 16;
       gs = -2;
       if (p < npv) {
@@ -239,7 +242,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   lds_sync();
   SDDM_STAMP(a, 3);
   // bias + noise embedding of this thread's 4 epilogue channels: in flight during the K loop
-  const int ec4 = (tid & 7) * 4;
+  const int ec4 = (tid & (TPP - 1)) * 4;
   float bb[4], sshift;
   {
     const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   }
   lds_sync();
 
-  constexpr int PPI = NT / 8;                            // pixels per epilogue pass
+  constexpr int PPI = NT / TPP;                          // pixels per epilogue pass
   constexpr int EIT = (MT + PPI - 1) / PPI;
   float sn = 0.f, s1[4], s2[4];
 #pragma unroll
@@ -335,7 +338,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   T* out = (T*)a.out + (size_t)b * img_out * a.Cout + n0 + ec4;
 #pragma unroll
   for (int it = 0; it < EIT; ++it) {
-    const int p = it * PPI + (tid >> 3);
+    const int p = it * PPI + tid / TPP;
     if (p < npv) {
       const int py = fdivi(p, rTW), px = p - py * a.TW;
       f32x4 s = *(const f32x4*)(red + p * NBP + ec4);
@@ -345,7 +348,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 #pragma unroll
       for (int i = 0; i < 4; ++i) d[i] = s[i];
       if (ident) {
-        const T* rp = (const T*)(smem + lay.rres) + p * 32 + ec4;
+        const T* rp = (const T*)(smem + lay.rres) + p * NB + ec4;
 #pragma unroll
         for (int i = 0; i < 4; ++i) d[i] += to_f32<T>(rp[i]);
       }
@@ -360,15 +363,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   }
   SDDM_STAMP(a, 5);
   if (a.stats && !(a.dbg & 16)) {
-    // lanes l and l + 8 of a DPP row hold the same 4 channels (row_ror:8 add), then the 4 rows of
-    // every wave through LDS, summed by one thread per channel
-    const float tn = sn + dpp_f32<0x128>(sn);
+    // the lanes of a DPP row holding the same 4 channels (16 / TPP of them, TPP apart) add by
+    // row rotations, then the 4 rows of every wave through LDS, summed by one thread per channel
+    auto rowred = [](float x) {
+      if constexpr (TPP == 4) x += dpp_f32<0x124>(x);   // row_ror:4
+      return x + dpp_f32<0x128>(x);                    // row_ror:8
+    };
+    const float tn = rowred(sn);
     float t1[4], t2[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { t1[i] = s1[i] + dpp_f32<0x128>(s1[i]); t2[i] = s2[i] + dpp_f32<0x128>(s2[i]); }
+    for (int i = 0; i < 4; ++i) { t1[i] = rowred(s1[i]); t2[i] = rowred(s2[i]); }
     lds_sync();                                        // red reads done
     float* xs = red;                                   // [NW * 4 rows][NB channels][3]
-    if ((lane & 15) < 8)
+    if ((lane & 15) < TPP)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float* e = xs + ((wave * 4 + (lane >> 4)) * NB + ec4 + i) * 3;
@@ -400,23 +407,23 @@ static int deep_ring(int steps_per_wave) {
   return 12;
 }
 
-template <typename T, bool S2, int MT, int NW>
+template <typename T, bool S2, int MT, int NW, int NB>
 static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   const int nck = (a.CA + a.CB) / 32, rck = a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0;
   const DeepGeo geo = deep_geo(S2, a.TR, a.TW, MT);
-  const DeepLds lay = deep_layout<T, MT, NW>(geo, nck, rck, a.CA + a.CB, a.res_mode == 1);
+  const DeepLds lay = deep_layout<T, MT, NW, NB>(geo, nck, rck, a.CA + a.CB, a.res_mode == 1);
   if (lo) {
     *lo = (size_t)lay.total;
     return hipSuccess;
   }
-  if (a.TR * a.TW > MT || a.Cout % 32 || (a.CA + a.CB) % 32 || (a.CA + a.CB) > 1000 || (a.RCA + a.RCB) % 32)
+  if (a.TR * a.TW > MT || a.Cout % NB || (a.CA + a.CB) % 32 || (a.CA + a.CB) > 1000 || (a.RCA + a.RCB) % 32)
     return hipErrorInvalidValue;
   if (lay.total > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid(a.n_tiles, B, a.Cout / 32), blk(64 * NW);
+  const dim3 grid(a.n_tiles, B, a.Cout / NB), blk(64 * NW);
   const int D = deep_ring<T, MT, NW>((nck * 9 + rck + NW - 1) / NW);
 #define SDDM_RING(DV)                                                                         \
   if (D == DV) {                                                                              \
-    hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT, NW, DV>), grid, blk, lay.total, s, a);   \
+    hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT, NW, DV, NB>), grid, blk, lay.total, s, a); \
     return hipGetLastError();                                                                 \
   }
   if constexpr (sizeof(T) == 4) {
@@ -430,32 +437,36 @@ static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   return hipErrorInvalidValue;
 }
 
+// nb: output channels per block (32, or 16 for twice the blocks with half the weights each)
 template <typename T>
-static hipError_t deep_dispatch(int mt, int nw, bool s2, const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
-#define SDDM_DEEP(S2V, MTV, NWV) \
-  if (s2 == S2V && mt == MTV && nw == NWV) return deep_go<T, S2V, MTV, NWV>(a, B, s, lo);
-  SDDM_DEEP(false, 32, 4) SDDM_DEEP(false, 64, 4) SDDM_DEEP(false, 128, 4)
-  SDDM_DEEP(true, 32, 4) SDDM_DEEP(true, 64, 4) SDDM_DEEP(true, 128, 4)
-  SDDM_DEEP(false, 32, 8) SDDM_DEEP(false, 64, 8) SDDM_DEEP(false, 128, 8)
-  SDDM_DEEP(true, 32, 8) SDDM_DEEP(true, 64, 8) SDDM_DEEP(true, 128, 8)
+static hipError_t deep_dispatch(int mt, int nw, int nb, bool s2, const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
+#define SDDM_DEEP(S2V, MTV, NWV, NBV) \
+  if (s2 == S2V && mt == MTV && nw == NWV && nb == NBV) return deep_go<T, S2V, MTV, NWV, NBV>(a, B, s, lo);
+  SDDM_DEEP(false, 32, 4, 32) SDDM_DEEP(false, 64, 4, 32) SDDM_DEEP(false, 128, 4, 32)
+  SDDM_DEEP(true, 32, 4, 32) SDDM_DEEP(true, 64, 4, 32) SDDM_DEEP(true, 128, 4, 32)
+  SDDM_DEEP(false, 32, 8, 32) SDDM_DEEP(false, 64, 8, 32) SDDM_DEEP(false, 128, 8, 32)
+  SDDM_DEEP(true, 32, 8, 32) SDDM_DEEP(true, 64, 8, 32) SDDM_DEEP(true, 128, 8, 32)
+  SDDM_DEEP(false, 16, 4, 16) SDDM_DEEP(false, 32, 4, 16) SDDM_DEEP(false, 64, 4, 16) SDDM_DEEP(false, 128, 4, 16)
+  SDDM_DEEP(true, 16, 4, 16) SDDM_DEEP(true, 32, 4, 16) SDDM_DEEP(true, 64, 4, 16)
+  SDDM_DEEP(false, 32, 8, 16) SDDM_DEEP(false, 64, 8, 16) SDDM_DEEP(false, 128, 8, 16)
 #undef SDDM_DEEP
   if (lo) *lo = (size_t)1 << 40;
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B, hipStream_t s) {
-  const int nw = a.deep_nw;
-  if (dtype == DT_F32) return deep_dispatch<float>(mt, nw, s2, a, B, s, nullptr);
-  if (dtype == DT_BF16) return deep_dispatch<bf16_t>(mt, nw, s2, a, B, s, nullptr);
-  return deep_dispatch<f16_t>(mt, nw, s2, a, B, s, nullptr);
+  const int nw = a.deep_nw, nb = a.deep_nb ? a.deep_nb : 32;
+  if (dtype == DT_F32) return deep_dispatch<float>(mt, nw, nb, s2, a, B, s, nullptr);
+  if (dtype == DT_BF16) return deep_dispatch<bf16_t>(mt, nw, nb, s2, a, B, s, nullptr);
+  return deep_dispatch<f16_t>(mt, nw, nb, s2, a, B, s, nullptr);
 }
 
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a) {
   size_t lo = (size_t)1 << 40;
-  const int nw = a.deep_nw;
-  if (dtype == DT_F32) (void)deep_dispatch<float>(mt, nw, s2, a, 1, 0, &lo);
-  else if (dtype == DT_BF16) (void)deep_dispatch<bf16_t>(mt, nw, s2, a, 1, 0, &lo);
-  else (void)deep_dispatch<f16_t>(mt, nw, s2, a, 1, 0, &lo);
+  const int nw = a.deep_nw, nb = a.deep_nb ? a.deep_nb : 32;
+  if (dtype == DT_F32) (void)deep_dispatch<float>(mt, nw, nb, s2, a, 1, 0, &lo);
+  else if (dtype == DT_BF16) (void)deep_dispatch<bf16_t>(mt, nw, nb, s2, a, 1, 0, &lo);
+  else (void)deep_dispatch<f16_t>(mt, nw, nb, s2, a, 1, 0, &lo);
   return lo;
 }
 

@@ -71,6 +71,7 @@ struct ConvArgs {
   float* stats;               // [B][n_tiles][Cout][2] (sum, M2 about tile mean) or null
   int ck_batch;               // (unused: conv_deep stages every input chunk at once)
   int deep_nw;                // conv_deep: waves per block (4: two blocks per CU, 8: one)
+  int deep_nb;                // conv_deep: output channels per block (32 or 16; 0 = 32)
   unsigned long long* stamps; // SDDM_STAMPS builds only: per-block phase timestamps [blocks][8]
   int dbg;                    // ablation flags for timing experiments (0 in production); conv_deep: 1 no GN
                               // finalize, 2 no GN+SiLU, 4 no staging loads, 8 no K loop, 16 no stats, 32 no weight loads

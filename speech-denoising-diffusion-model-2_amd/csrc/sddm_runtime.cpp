@@ -292,7 +292,7 @@ struct sddm_ctx {
   // dtype / num_samples (sddm_set_conv_tuning)
   std::map<std::string, std::pair<int, int>> deep_tune;
   // per-layer kernel choice: 1 strip, 2 tile (a = configuration), 3 deep (a = pixels, b = waves)
-  struct KernTune { int kind, a, b; };
+  struct KernTune { int kind, a, b, c; };
   std::map<std::string, KernTune> kern_tune;
   int tune_B = -1, tune_dtype = -1, tune_N = -1;
   int hop_samples = 256;
@@ -490,7 +490,7 @@ static int upload_tables(sddm_ctx* c) {
 struct ConvChoice {
   int strip = 0;      // 1: row-streaming kernel (conv_strip.hip), 0: whole-K tile kernel (conv_deep.hip)
   int nblk = 32, SR = 0, mpi = 128;
-  int mt = 0, ckb = 0, nw = 4;                    // conv_deep: pixels per block, input chunks, waves
+  int mt = 0, ckb = 0, nw = 4, nb = 32;           // conv_deep: pixels per block, input chunks, waves, channels
   int tile = -1;                                  // conv_tile configuration (16-bit dtypes), -1: none
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
 };
@@ -500,16 +500,24 @@ struct ConvChoice {
 // (256 CUs x 2 blocks at 4 waves, x 1 block at 8 waves); among equal round counts 8 waves (the
 // K split 8 ways, weights resident) and then the smaller tile (less work per block) win.
 // SDDM_DEEP_CFG=mt:nw forces one configuration wherever it fits (experiments).
-static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int want_mt = 0, int want_nw = 0) {
-  const int nz = a.Cout / 32;
-  static int force_mt = -1, force_nw = -1;
+static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int want_mt = 0, int want_nw = 0,
+                        int want_nb = 0) {
+  static int force_mt = -1, force_nw = -1, force_nb = 0;
   if (force_mt < 0) {
     force_mt = force_nw = 0;
-    if (const char* e = std::getenv("SDDM_DEEP_CFG")) std::sscanf(e, "%d:%d", &force_mt, &force_nw);
+    if (const char* e = std::getenv("SDDM_DEEP_CFG")) std::sscanf(e, "%d:%d:%d", &force_mt, &force_nw, &force_nb);
   }
+  // 16-channel blocks only where asked for (tuning table or SDDM_DEEP_CFG): twice the blocks, each
+  // with half the weight bytes (the per-CU load volume bounds these layers) but the input halo
+  // transformed twice as often
+  const int nb = want_mt ? (want_nb ? want_nb : 32) : (force_nb ? force_nb : 32);
+  if (a.Cout % nb) return false;
+  const int nz = a.Cout / nb;
+  a.deep_nb = nb;
   struct Cand { int mt, nw, TR, TW, tiles_x, n_tiles, blocks, rounds; };
   std::vector<Cand> cs;
-  for (int mt : {128, 64, 32}) {
+  for (int mt : {128, 64, 32, 16}) {
+    if (mt == 16 && nb != 16) continue;
     const int TW = std::min(a.Wo, mt);
     if (mt % TW || a.Wo % TW) continue;
     const int TR = std::min(mt / TW, a.Ho);
@@ -536,7 +544,7 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
       if (c.mt < pick->mt) pick = &c;
     }
   }
-  ch.strip = 0; ch.mt = pick->mt; ch.nw = pick->nw; ch.ckb = (a.CA + a.CB) / 32;
+  ch.strip = 0; ch.mt = pick->mt; ch.nw = pick->nw; ch.nb = nb; ch.ckb = (a.CA + a.CB) / 32;
   ch.TR = pick->TR; ch.TW = pick->TW; ch.tiles_x = pick->tiles_x; ch.n_tiles = pick->n_tiles;
   return true;
 }
@@ -585,7 +593,7 @@ static bool choose_tile(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
 }
 
 static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
-                        ConvChoice& ch, int want_mt = 0, int want_nw = 0, int kind = 0, int ka = 0) {
+                        ConvChoice& ch, int want_mt = 0, int want_nw = 0, int kind = 0, int ka = 0, int want_nb = 0) {
   ConvArgs a{};
   a.CA = Cin; a.CB = 0; a.RCA = RC; a.RCB = 0; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout;
   a.upsample = up ? 1 : 0;
@@ -623,7 +631,7 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
     }
   }
   if (want_mt == 0 && kind != 3 && choose_tile(dt, B, a, s2, ch)) return true;
-  return choose_deep(dt, B, a, s2, ch, want_mt, want_nw);
+  return choose_deep(dt, B, a, s2, ch, want_mt, want_nw, want_nb);
 }
 
 static int build_lane(sddm_ctx* c, Lane& L) {
@@ -679,17 +687,17 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   const bool tuned = c->tune_B == PB && c->tune_dtype == dt && c->tune_N == N;
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
-    int wm = 0, wn = 0, kind = 0, ka = 0;
+    int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;
     if (tuned) {
       auto it = c->deep_tune.find(name);
       if (it != c->deep_tune.end()) { wm = it->second.first; wn = it->second.second; kind = 3; }
       auto kt = c->kern_tune.find(name);
       if (kt != c->kern_tune.end()) {
         kind = kt->second.kind; ka = kt->second.a;
-        if (kind == 3) { wm = kt->second.a; wn = kt->second.b; }
+        if (kind == 3) { wm = kt->second.a; wn = kt->second.b; wb = kt->second.c; }
       }
     }
-    return choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka);
+    return choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka, wb);
   };
   const int TRin = 512 / W;
   if (u.inner != 32 || 512 % W || F % TRin || (TRin + 1) * S + W + 2 > 1024)
@@ -847,7 +855,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           int nb = 32;
           if (ch.tile >= 0) { const TileCfg tc = conv_tile_cfg(ch.tile); nb = tc.wco * tc.fc * 16; }
           c->stamp_blocks = ch.strip ? (int64_t)(a.Ho / ch.SR) * B * ((a.Cout + ch.nblk - 1) / ch.nblk)
-                                     : (int64_t)a.n_tiles * B * (a.Cout / nb);
+                                     : (int64_t)a.n_tiles * B * (a.Cout / (ch.tile >= 0 ? nb : ch.nb));
         }
       }
 #endif
@@ -861,9 +869,10 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           }
                           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
                           if (ch.tile >= 0) return launch_conv_tile(dt, ch.tile, s2, x, B, s);
-                          x.ck_batch = ch.ckb; x.deep_nw = ch.nw;
+                          x.ck_batch = ch.ckb; x.deep_nw = ch.nw; x.deep_nb = ch.nb;
                           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
-                        }, st.w + (ch.strip ? "[strip]" : (ch.tile >= 0 ? "[tile" + std::to_string(ch.tile) + "]" : ""))});
+                        }, st.w + (ch.strip ? "[strip]" : (ch.tile >= 0 ? "[tile" + std::to_string(ch.tile) + "]"
+                                                                         : "[deep" + std::to_string(ch.mt) + "_" + std::to_string(ch.nw) + "_" + std::to_string(ch.nb) + "]"))});
       {
         char kn[160];
         if (ch.strip)
@@ -873,7 +882,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           snprintf(kn, sizeof(kn), "conv_tile_kernel<%s,%d,%d,%d,%d,%d> (tile%d)", dt_name(dt), s2 ? 1 : 0, tc.wpx, tc.wco,
                    tc.fp, tc.fc, ch.tile);
         } else
-          snprintf(kn, sizeof(kn), "conv_deep_kernel<%s,%d,%d,%d>", dt_name(dt), s2 ? 1 : 0, ch.mt, ch.nw);
+          snprintf(kn, sizeof(kn), "conv_deep_kernel<%s,%d,%d,%d,%d>", dt_name(dt), s2 ? 1 : 0, ch.mt, ch.nw, ch.nb);
         L.ops.back().kname = kn;
       }
       {  // flags: 1 no stats, 2 no GroupNorm transform, 4 no residual / embedding, 8 skip the K loop
@@ -888,7 +897,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           x.dbg = fl;
           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
           if (ch.tile >= 0) return launch_conv_tile(dt, ch.tile, s2, x, B, s);
-          x.ck_batch = ch.ckb; x.deep_nw = ch.nw;
+          x.ck_batch = ch.ckb; x.deep_nw = ch.nw; x.deep_nb = ch.nb;
           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
         };
         (void)base;
@@ -1504,16 +1513,16 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
       if (kv.second.kind != Json::ARR || kv.second.arr.size() != 2) FAIL(SDDM_ERR_INVALID_ARG, "deep.%s: [mt, nw]", kv.first.c_str());
       c->deep_tune[kv.first] = {(int)kv.second.arr[0].num, (int)kv.second.arr[1].num};
     }
-  // "kernel": {"<layer>": "strip" | "tile:<cfg>" | "deep" | "deep:<mt>:<nw>"}
+  // "kernel": {"<layer>": "strip" | "tile:<cfg>" | "deep" | "deep:<mt>:<nw>[:<nb>]"}
   if (j.has("kernel"))
     for (const auto& kv : j.at("kernel").obj) {
       if (kv.second.kind != Json::STR) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: a string", kv.first.c_str());
       const std::string& v = kv.second.str;
-      sddm_ctx::KernTune t{0, 0, 0};
+      sddm_ctx::KernTune t{0, 0, 0, 0};
       if (v == "strip") t.kind = 1;
       else if (v.rfind("tile:", 0) == 0) { t.kind = 2; t.a = std::atoi(v.c_str() + 5); }
       else if (v == "deep") t.kind = 3;
-      else if (v.rfind("deep:", 0) == 0) { t.kind = 3; std::sscanf(v.c_str() + 5, "%d:%d", &t.a, &t.b); }
+      else if (v.rfind("deep:", 0) == 0) { t.kind = 3; std::sscanf(v.c_str() + 5, "%d:%d:%d", &t.a, &t.b, &t.c); }
       else FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: unknown choice '%s'", kv.first.c_str(), v.c_str());
       if (t.kind == 2 && (t.a < 0 || t.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), t.a);
       c->kern_tune[kv.first] = t;

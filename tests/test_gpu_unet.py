@@ -91,8 +91,18 @@ _TUNING = {"downs.4": "tile:2", "downs.5.block1": "tile:10", "downs.5.block2": "
            "ups.11.block1": "tile:1", "ups.12.block1": "strip"}
 
 
+# conv_deep with 16-channel blocks: every pixel tile (16..128), both wave counts, stride 2,
+# upsample, virtual concat, identity residual and res_conv chunks
+_TUNING16 = {"downs.7.block1": "deep:64:8:16", "downs.7.block2": "deep:128:4:16", "downs.8": "deep:32:4:16",
+             "downs.9.block1": "deep:32:8:16", "downs.9.block2": "deep:16:4:16", "downs.10": "deep:16:4:16",
+             "mid.0.block1": "deep:16:4:16", "mid.0.block2": "deep:32:4:16", "ups.0.block1": "deep:32:8:16",
+             "ups.0.block2": "deep:16:4:16", "ups.1": "deep:64:4:16", "ups.4": "deep:128:8:16",
+             "ups.5.block1": "deep:64:8:16", "ups.6.block2": "deep:128:4:16"}
+
+
 @pytest.mark.parametrize("dtype,tol,tuned", [("float32", 1e-4, None), ("bfloat16", 2.5e-2, None),
                                             ("bfloat16", 2.5e-2, "table"), ("bfloat16", 2.5e-2, "repo"),
+                                            ("bfloat16", 2.5e-2, "table16"), ("float32", 1e-4, "table16"),
                                             ("float16", 5e-3, None)])
 def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     """B=16 x N=16448 (the bench shape), 16 distinct rows at 16 noise levels: the kernels and tiles
@@ -104,8 +114,9 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     cond, x_t, nl, ref = bench_rows(N, B)
     dev = torch_cuda.device("cuda", 0)
     ctx = make_ctx(N, dtype)
-    if tuned == "table":
-        ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N, "kernel": _TUNING})
+    if tuned in ("table", "table16"):
+        ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N,
+                             "kernel": _TUNING if tuned == "table" else _TUNING16})
     elif tuned == "repo":
         path = os.path.join(os.path.dirname(sddm_hip.__file__), "..", "configs", "conv_tuning.json")
         if not os.path.exists(path):

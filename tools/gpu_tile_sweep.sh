@@ -13,4 +13,9 @@ for c in 0 1 2 3 4 5 6 7 8 9 10 11; do
 SDDM_TILE_CFG=$c timeout -k 10 120 python tools/profile_ops.py --timesteps 10 --json gpurun_out/sweep/t$c.json > gpurun_out/sweep/t$c.log 2>&1 || { echo FAIL_$c; tail -5 gpurun_out/sweep/t$c.log; exit 1; }
 echo "cfg $c: $(head -2 gpurun_out/sweep/t$c.log | tail -1)"
 done
+for dc in 16:4:16 32:4:16 32:8:16 64:4:16 64:8:16 128:8:16 128:4:16 32:8:32 64:8:32 128:8:32 64:4:32 128:4:32 32:4:32; do
+n=$(echo $dc | tr ':' '_')
+SDDM_NO_TILE=1 SDDM_DEEP_CFG=$dc timeout -k 10 120 python tools/profile_ops.py --timesteps 10 --json gpurun_out/sweep/d$n.json > gpurun_out/sweep/d$n.log 2>&1 || { echo FAIL_d$n; tail -5 gpurun_out/sweep/d$n.log; exit 1; }
+echo "deep $dc: $(head -2 gpurun_out/sweep/d$n.log | tail -1)"
+done
 echo ALL_OK

@@ -26,13 +26,15 @@ print(f"step total: deep {tot_deep:.1f}  auto {tot_auto:.1f}  best-per-layer {to
 if len(sys.argv) > 2:       # write the per-layer table for sddm_set_conv_tuning
     kern = {}
     for L, name in pick.items():
-        m = re.search(r"\[(\w+?)(\d*)\]", name)
+        m = re.search(r"\[(strip|tile(\d+)|deep(\d+)_(\d+)_(\d+))\]", name)
         if m is None:
             kern[L] = "deep"
         elif m.group(1) == "strip":
             kern[L] = "strip"
-        elif m.group(1) == "tile":
+        elif m.group(2) is not None:
             kern[L] = "tile:" + m.group(2)
+        else:
+            kern[L] = "deep:%s:%s:%s" % (m.group(3), m.group(4), m.group(5))
     if "downs.0" in kern:
         del kern["downs.0"]
     kern.pop("final_conv", None)
