@@ -198,18 +198,23 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
       wh[fc][j] = (f16_t)v;
       wl[fc][j] = (f16_t)(v - (float)wh[fc][j]);
     }
-  float st1[2][4], st2[2][4];
+  f32x2 st1[2][2], st2[2][2], bp[2][2];                  // packed pairs (accumulator register pairs)
 #pragma unroll
   for (int fc = 0; fc < 2; ++fc)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) { st1[fc][i] = 0.f; st2[fc][i] = 0.f; }
+    for (int h = 0; h < 2; ++h) {
+      st1[fc][h] = f32x2{0.f, 0.f};
+      st2[fc][h] = f32x2{0.f, 0.f};
+      bp[fc][h] = f32x2{bias[fc][2 * h], bias[fc][2 * h + 1]};
+    }
+  const float rW = 1.0f / (float)W;
   __syncthreads();                                        // frame image staged
   SDDM_STAMP(a, 1);
   const float* imgf = &img[0][0];
 #pragma unroll 2
   for (int fr = 0; fr < NFR; ++fr) {
     const int p = wave * (NFR * 16) + fr * 16 + (lane & 15);
-    const int r = p / W, w = p - r * W;
+    const int r = fdivi(p, rW), w = p - r * W;
     const int pb = r * IW + w;                              // image index of tap (0, 0)
     float xv[KPL];
 #pragma unroll
@@ -248,14 +253,12 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
 #pragma unroll
     for (int fc = 0; fc < 2; ++fc) {
       // statistics of the fp32 values about the shift = bias (common to the whole tile)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float d = acc[fc][i];
-        st1[fc][i] += d;
-        st2[fc][i] += d * d;
-      }
-      store4<T>(op + fc * 16 + 4 * g, acc[fc][0] + bias[fc][0], acc[fc][1] + bias[fc][1], acc[fc][2] + bias[fc][2],
-                acc[fc][3] + bias[fc][3]);
+      const f32x2 d0 = f32x2{acc[fc][0], acc[fc][1]}, d1 = f32x2{acc[fc][2], acc[fc][3]};
+      st1[fc][0] += d0;
+      st1[fc][1] += d1;
+      st2[fc][0] = __builtin_elementwise_fma(d0, d0, st2[fc][0]);
+      st2[fc][1] = __builtin_elementwise_fma(d1, d1, st2[fc][1]);
+      store4p<T>(op + fc * 16 + 4 * g, d0 + bp[fc][0], d1 + bp[fc][1]);
     }
   }
   SDDM_STAMP(a, 2);
@@ -264,11 +267,11 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   for (int fc = 0; fc < 2; ++fc)
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      st1[fc][i] = row_sum16(st1[fc][i]);                   // DPP row adds (VALU)
-      st2[fc][i] = row_sum16(st2[fc][i]);
+      const float t1 = row_sum16(st1[fc][i >> 1][i & 1]);    // DPP row adds (VALU)
+      const float t2 = row_sum16(st2[fc][i >> 1][i & 1]);
       if ((lane & 15) == 0) {
-        xs_red[wave][fc * 16 + 4 * g + i][0] = st1[fc][i];
-        xs_red[wave][fc * 16 + 4 * g + i][1] = st2[fc][i];
+        xs_red[wave][fc * 16 + 4 * g + i][0] = t1;
+        xs_red[wave][fc * 16 + 4 * g + i][1] = t2;
       }
     }
   lds_sync();                                              // (the output stores stay in flight)
@@ -362,9 +365,10 @@ __global__ __launch_bounds__(256) void init_state_kernel(InitArgs a) {
 //  phase 3: overlapAdd in ascending frame order (UNetModified2.py:37-39) and p_transition, four
 //           consecutive samples per thread (one Philox counter group).
 // =============================================================================================
-template <typename T>
-__global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
+template <typename T, int NT>
+__global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NWV = NT / 64;                // waves per block
   const int b = blockIdx.y, f0 = blockIdx.x * a.FT, tid = threadIdx.x;
   const int C = a.C, W = a.W, S = a.S, F = a.F;
   const int back = W / S - 1;                 // extra frames before f0 needed by the OLA
@@ -397,18 +401,22 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
   const int npos = PR * PC, nfr = (npos + 15) / 16;
   // every fragment of this wave is loaded before the first is used (one memory latency, not one
   // per fragment): FRW fragments per pass
-  constexpr int NWV = 8, FRW = 12;                   // waves per block, fragments per wave and pass
+  constexpr int FRW = 12;                            // fragments per wave and pass
   constexpr int NV = (int)sizeof(T) * 8 / 16;        // 16-byte vectors per 8 channels
   typedef T vec8 __attribute__((ext_vector_type(8)));
   f32x4 xr[FRW][NV];
+  unsigned inmask = 0;                               // bit q: fragment q's position is inside the image
+  const float rPC = 1.0f / (float)PC;                // positions < 2^21: fdivi is exact
   auto load_pass = [&](int fr0) {
+    inmask = 0;
 #pragma unroll
     for (int q = 0; q < FRW; ++q) {
       const int pp = (fr0 + NWV * q) * 16 + (lane & 15);
-      const int r = pp / PC, col = pp - r * PC;
+      const int r = fdivi(pp, rPC), col = pp - r * PC;
       const int f = f0 - back - 1 + r, w = col - 1;
       const bool in = pp < npos && f >= 0 && f < F && w >= 0 && w < W;
-      const size_t off = in ? ((size_t)f * W + w) * C + 8 * g : 8 * g;
+      inmask |= in ? 1u << q : 0u;
+      const int off = in ? (f * W + w) * C + 8 * g : 8 * g;   // < 2^31 elements per image
 #pragma unroll
       for (int h = 0; h < NV; ++h) xr[q][h] = *(const f32x4*)((const char*)(src + off) + 16 * h);
     }
@@ -417,13 +425,16 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
   gl.finish(gf, b, C, 0, gs, gs + C);
   lds_sync();                                        // scale / shift visible (loads stay in flight)
   SDDM_STAMP(a, 1);
+  // SiLU through exp2 with the constants folded: t = -(x sc + sh) log2(e) = x sc' + sh', and
+  // silu = -ln2 * t / (1 + 2^t); the -ln2 goes into the fp32 weights (one multiply per lane)
+  constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
   float wv[8], sc[8], sh[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = 8 * g + j;
-    wv[j] = tapr < 9 ? a.w[c * 9 + tapr] : 0.f;
-    sc[j] = gs[c];
-    sh[j] = gs[C + c];
+    wv[j] = tapr < 9 ? a.w[c * 9 + tapr] * -kLN2 : 0.f;
+    sc[j] = gs[c] * -kL2E;
+    sh[j] = gs[C + c] * -kL2E;
   }
   for (int fr0 = wave; fr0 < nfr; fr0 += NWV * FRW) {
   if (fr0 != wave) load_pass(fr0);                   // inputs larger than one pass
@@ -431,17 +442,18 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
   for (int q = 0; q < FRW; ++q) {
     const int fr = fr0 + NWV * q;
     const int pp = fr * 16 + (lane & 15);
-    const int r = pp / PC, col = pp - r * PC;
-    const int f = f0 - back - 1 + r, w = col - 1;
-    const bool in = fr < nfr && pp < npos && f >= 0 && f < F && w >= 0 && w < W;
-    const vec8 x = __builtin_bit_cast(vec8, xr[q]);
+    const int r = fdivi(pp, rPC), col = pp - r * PC;
+    const bool in = (inmask >> q) & 1u;               // zero padding: the position's column of the
+    const vec8 x = __builtin_bit_cast(vec8, xr[q]);   // product is masked, not its 8 inputs
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; j += 2) {
-      const f32x2 o = silu2(f32x2{to_f32<T>(x[j]), to_f32<T>(x[j + 1])} * f32x2{sc[j], sc[j + 1]} +
-                            f32x2{sh[j], sh[j + 1]});
-      v[j] = in ? o.x : 0.f;
-      v[j + 1] = in ? o.y : 0.f;
+      const f32x2 t = __builtin_elementwise_fma(f32x2{to_f32<T>(x[j]), to_f32<T>(x[j + 1])}, f32x2{sc[j], sc[j + 1]},
+                                                f32x2{sh[j], sh[j + 1]});
+      const f32x2 d = f32x2{__builtin_amdgcn_exp2f(t.x), __builtin_amdgcn_exp2f(t.y)} + f32x2{1.f, 1.f};
+      const f32x2 o = t * f32x2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+      v[j] = o.x;
+      v[j + 1] = o.y;
     }
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if constexpr (sizeof(T) == 4) {
@@ -461,15 +473,17 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
         acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc, 0, 0, 0);
       }
     }
+    // a lane's MFMA output column is its own position (lane & 15), all taps of it: padding
+    // positions store 0 (outside the image), positions past the halo store nothing
     if (fr < nfr && pp < npos)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        if (4 * g + i < 9) P[((4 * g + i) * PR + r) * PC + col] = acc[i];
+        if (4 * g + i < 9) P[((4 * g + i) * PR + r) * PC + col] = in ? acc[i] : 0.f;
   }
   }
   lds_sync();
   SDDM_STAMP(a, 2);
-  for (int p = tid; p < YR * W; p += blockDim.x) {
+  for (int p = tid; p < YR * W; p += NT) {
     const int r = p / W, w = p - r * W;        // y row r <-> P rows r .. r+2, cols w .. w+2
     float s = 0.f;
 #pragma unroll
@@ -489,21 +503,42 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
     f32x4 z = {0.f, 0.f, 0.f, 0.f};
     const bool aligned = (e0 & 3) == 0;
     if (a.mode >= 0 && t > 1 && aligned) z = philox_normal4(seed, (uint32_t)t, e0 >> 2);
+    f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
+    if ((S & 3) == 0 && (W & 3) == 0) {
+      // overlapAdd of 4 consecutive samples: with S and W multiples of 4 they are covered by the
+      // same frames [flo, fhi], so the frame range is computed once (float-reciprocal division,
+      // n4 < 2^21) and each frame contributes one 16-byte LDS read; ascending frame order as
+      // UNetModified2.py:37-39
+      const float rS = 1.0f / (float)S;
+      const int fhi = min(F - 1, fdivi(n4, rS));
+      const int flo = n4 - W + 1 <= 0 ? 0 : fdivi(n4 - W + S, rS);
+      for (int f = flo; f <= fhi; ++f) e4 += *(const f32x4*)(y + (f - (f0 - back)) * W + (n4 - f * S));
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n4 + j;
-      if (n >= n_end) break;
-      int flo = (n - W + S) / S;
-      if (n - W + 1 <= 0) flo = 0;
-      const int fhi = min(F - 1, n / S);
-      float e = 0.f;
-      for (int f = flo; f <= fhi; ++f) e += y[(f - (f0 - back)) * W + (n - f * S)];
-      if (a.mode < 0) {
-        a.eps_out[(size_t)b * a.N + n] = e;
-      } else {
-        const float zz = (t > 1) ? (aligned ? z[j] : philox_normal1(seed, (uint32_t)t, e0 + j)) : 0.f;
-        xrow[n] = transition_one(a.mode, a.co, t, xin[j], e, a.cond ? cin[j] : 0.f, zz);
+      for (int j = 0; j < 4; ++j) {
+        const int n = n4 + j;
+        int flo = (n - W + S) / S;
+        if (n - W + 1 <= 0) flo = 0;
+        const int fhi = min(F - 1, n / S);
+        float e = 0.f;
+        for (int f = flo; f <= fhi; ++f) e += y[(f - (f0 - back)) * W + (n - f * S)];
+        e4[j] = e;
       }
+    }
+    if (a.mode < 0) {
+      if (n4 + 3 < n_end) *(f32x4*)(a.eps_out + (size_t)b * a.N + n4) = e4;
+      else
+        for (int j = 0; j < 4 && n4 + j < n_end; ++j) a.eps_out[(size_t)b * a.N + n4 + j] = e4[j];
+    } else {
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float zz = (t > 1) ? (aligned ? z[j] : philox_normal1(seed, (uint32_t)t, e0 + j)) : 0.f;
+        o[j] = transition_one(a.mode, a.co, t, xin[j], e4[j], a.cond ? cin[j] : 0.f, zz);
+      }
+      if (n4 + 3 < n_end) *(f32x4*)(xrow + n4) = o;
+      else
+        for (int j = 0; j < 4 && n4 + j < n_end; ++j) xrow[n4 + j] = o[j];
     }
   }
   SDDM_STAMP(a, 6);
@@ -513,12 +548,19 @@ __global__ __launch_bounds__(512) void final_kernel(FinalArgs a) {
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
   const int back = a.W / a.S - 1, YR = a.FT + back;
   const size_t lds = ((size_t)9 * (YR + 2) * (a.W + 2) + (size_t)YR * a.W + 2 * a.C) * 4;
-  // one pass of 4 samples per thread covers a block's samples (the last block's tail included)
-  if (lds > 160 * 1024 || a.F % a.FT || a.C != 32 || a.FT * a.S + a.W > 4 * 512 || a.N % 4) return hipErrorInvalidValue;
+  // 16-frame tiles as one 16-wave block per CU (less halo re-transform than 8-frame tiles, and
+  // the whole grid resident in one round); one pass of 4 samples per thread covers a block's
+  // samples (the last block's tail included)
+  const int nt = a.FT >= 16 ? 1024 : 512;
+  if (lds > 160 * 1024 || a.F % a.FT || a.C != 32 || a.FT * a.S + a.W > 4 * nt || a.N % 4) return hipErrorInvalidValue;
   dim3 grid(a.F / a.FT, B);
-  if (dtype == DT_F32) hipLaunchKernelGGL(final_kernel<float>, grid, dim3(512), lds, s, a);
-  else if (dtype == DT_BF16) hipLaunchKernelGGL(final_kernel<bf16_t>, grid, dim3(512), lds, s, a);
-  else hipLaunchKernelGGL(final_kernel<f16_t>, grid, dim3(512), lds, s, a);
+#define SDDM_FINAL(TT)                                                                    \
+  if (nt == 1024) hipLaunchKernelGGL((final_kernel<TT, 1024>), grid, dim3(1024), lds, s, a); \
+  else hipLaunchKernelGGL((final_kernel<TT, 512>), grid, dim3(512), lds, s, a);
+  if (dtype == DT_F32) { SDDM_FINAL(float) }
+  else if (dtype == DT_BF16) { SDDM_FINAL(bf16_t) }
+  else { SDDM_FINAL(f16_t) }
+#undef SDDM_FINAL
   return hipGetLastError();
 }
 

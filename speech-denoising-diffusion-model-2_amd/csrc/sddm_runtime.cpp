@@ -936,7 +936,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           x.sp = lp->rs.t_dev ? (const StepParams*)lp->rs.t_dev : nullptr;
                           return launch_final(dt, x, B, s);
                         }, "final_conv"});
-      L.ops.back().kname = std::string("final_kernel<") + dt_name(dt) + ">";
+      L.ops.back().kname = std::string("final_kernel<") + dt_name(dt) + (f.FT >= 16 ? ",1024>" : ",512>");
     }
   }
   return SDDM_OK;
