@@ -17,6 +17,8 @@
 //   3. the gated activation goes back to LDS (plane-major) and output_residual / output_projection
 //      run as one K = 64 GEMM; the epilogue writes (x + residual) / sqrt(2) to the other x buffer
 //      and accumulates the skip sum in fp32.
+#include <cstdlib>
+
 #include "conv_common.h"
 #include "kernels.h"
 
@@ -27,6 +29,14 @@ constexpr int DW_MS = 128;          // samples per layer block
 
 __device__ __forceinline__ float dw_silu(float x) { return x * (1.0f / (1.0f + expf(-x))); }
 __device__ __forceinline__ float dw_sigmoid(float x) { return 1.0f / (1.0f + expf(-x)); }
+// gate activations from one exp2 and one reciprocal each (v_exp_f32 / v_rcp_f32, ~1 ulp):
+// sigmoid(x) = 1 / (1 + 2^(-x log2 e)), tanh(x) = 2 sigmoid(2x) - 1 (absolute error ~1e-7 near 0)
+__device__ __forceinline__ float dw_sigmoid_fast(float x) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -1.4426950408889634f));
+}
+__device__ __forceinline__ float dw_tanh_fast(float x) {
+  return 2.0f * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(x * -2.8853900817779268f)) - 1.0f;
+}
 
 // ---------------- noise-step embedding + diffusion projections of every layer ----------------
 __global__ __launch_bounds__(512) void dw_embed_kernel(DWEmbedArgs a) {
@@ -203,8 +213,10 @@ hipError_t launch_dw_input(int dtype, const DWInArgs& a, hipStream_t s) {
 }
 
 // ---------------- fused residual layer ----------------
-template <typename T>
-__global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
+// PREW: the 16-bit weight fragments held in registers for the whole block (236 VGPRs: two blocks
+// per CU); without, loaded per K step (three blocks per CU)
+template <typename T, bool PREW>
+__global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs a) {
   constexpr int ES = (int)sizeof(T), VE = 16 / ES;
   constexpr int UPS = DW_C / VE;                  // 16-byte units (planes) per sample and tap
   constexpr int PB = 64 / UPS;                    // samples per 64-unit staging group
@@ -217,12 +229,56 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int n0 = blockIdx.x * DW_MS, b = blockIdx.y, N = a.N, d = a.dil;
-  const T* xin = (const T*)a.x_in + (size_t)b * N * DW_C;
-  const int row = a.ds_per_b ? b : (a.t_dev ? *a.t_dev : 0);
-  const float* ds = a.ds + ((size_t)row * a.L + a.layer) * DW_C;
-
+  const int N = a.N, d = a.dil;
   const int cg = wave * 16 + 4 * g;               // gate row base; filter rows cg + 64
+  // both GEMMs' weight fragments and biases are issued first (16-bit weights: 14 fragments x 4
+  // VGPRs; fp32 fragments are twice that, so the fp32 path loads them per K step)
+  const T* w1 = (const T*)a.w1;
+  const T* w2 = (const T*)a.w2;
+  constexpr bool PRE = sizeof(T) == 2 && PREW;
+  auto w1frag = [&](int s, int c) {
+    return load_frag<T>((const char*)(w1 + (size_t)(c * 64 + wave * 16 + (lane & 15)) * 192 + s * 32 + g * 8));
+  };
+  auto w2frag = [&](int s) { return load_frag<T>((const char*)(w2 + (size_t)(wave * 16 + (lane & 15)) * DW_C + s * 32 + g * 8)); };
+  Frag<T> aw1[PRE ? 6 : 1][2], aw2[PRE ? 2 : 1];
+  if constexpr (PRE) {
+#pragma unroll
+    for (int s = 0; s < 6; ++s)
+#pragma unroll
+      for (int c = 0; c < 2; ++c) aw1[s][c] = w1frag(s, c);
+#pragma unroll
+    for (int s = 0; s < 2; ++s) aw2[s] = w2frag(s);
+  }
+  float bg[4], bfl[4], br[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { bg[i] = a.b1[cg + i]; bfl[i] = a.b1[cg + 64 + i]; br[i] = a.b2[cg + i]; }
+  const int t_now = a.t_dev ? *a.t_dev : 0;
+  {
+  const int b = blockIdx.y, n0 = blockIdx.x * DW_MS;
+  const T* xin = (const T*)a.x_in + (size_t)b * N * DW_C;
+  const float* ds = a.ds + ((size_t)(a.ds_per_b ? b : t_now) * a.L + a.layer) * DW_C;
+  // the diffusion projection of this thread's staging channels first (needed first: the loads
+  // issued after it stay in flight while the staging waits for it); the channel unit q of a
+  // staging unit depends on tid only (u = u0 + tid + 256 k with u0 a multiple of 256)
+  const int qs = (tid & 63) / PB;
+  float dsv[VE];
+#pragma unroll
+  for (int e = 0; e < VE; ++e) dsv[e] = ds[qs * VE + e];
+  // then every other load that does not depend on the staged image, so a tile waits on memory
+  // once: the conditioner rows of this lane's gate / filter channels (used after GEMM 1) and the
+  // residual x of its output channels (used in the epilogue); clamped, unconditional
+  vec4 cnd[2][8], xres[8];
+  {
+    const T* cb = (const T*)a.cond + (size_t)a.layer * a.B * N * 128;   // layer-major: one stream per layer
+#pragma unroll
+    for (int p = 0; p < 8; ++p) {
+      const int n = min(n0 + p * 16 + (lane & 15), N - 1);
+      const T* cp = cb + ((size_t)b * N + n) * 128;
+      cnd[0][p] = *(const vec4*)(cp + cg);
+      cnd[1][p] = *(const vec4*)(cp + cg + 64);
+      xres[p] = *(const vec4*)(xin + (size_t)n * DW_C + cg);
+    }
+  }
   // ---- 1. y = x + diffusion projection -> LDS ----
   // dilation <= 64: one window of rows n0 - d .. n0 + 127 + d (the three taps overlap; each x row
   // is read and transformed once), planes padded to 256 B; larger dilations: three disjoint tap
@@ -230,8 +286,8 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
   const bool win = d <= 64;
   const int ROWS = win ? (DW_MS + 2 * d + PB - 1) / PB * PB : DW_MS, TAPS = win ? 1 : 3;   // whole staging groups
   const int PL = win ? (ROWS * 16 + 255) / 256 * 256 : PLANE;
-  const int NUr = TAPS * ROWS * UPS;
-  for (int u0 = 0; u0 < NUr; u0 += MAXU * 256) {
+  const int NUr = TAPS * ROWS * UPS;             // 16-bit: <= MAXU * 256 (checked by the launcher)
+  auto stage_pass = [&](int u0) {
     f32x4 reg[MAXU];
     int dst[MAXU], qv[MAXU];
 #pragma unroll
@@ -243,46 +299,33 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
       const bool ok = n >= 0 && n < N && u0 + tid + k * 256 < NUr;
       reg[k] = *(const f32x4*)(xin + (size_t)min(max(n, 0), N - 1) * DW_C + q * VE);
       dst[k] = (u0 + tid + k * 256 < NUr) ? ((tap * UPS + q) * PL + s * 16) : -1;
-      qv[k] = ok ? q : -1;
+      qv[k] = ok ? 1 : 0;
     }
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
-      if (dst[k] < 0) continue;
       typedef T vec __attribute__((ext_vector_type(VE)));
       vec v = __builtin_bit_cast(vec, reg[k]);
-      const int q = qv[k];
 #pragma unroll
-      for (int e = 0; e < VE; ++e) v[e] = q >= 0 ? from_f32<T>(to_f32<T>(v[e]) + ds[q * VE + e]) : from_f32<T>(0.f);
-      *(f32x4*)(yin + dst[k]) = __builtin_bit_cast(f32x4, v);
+      for (int e = 0; e < VE; ++e) v[e] = from_f32<T>(qv[k] ? to_f32<T>(v[e]) + dsv[e] : 0.f);
+      if (dst[k] >= 0) *(f32x4*)(yin + dst[k]) = __builtin_bit_cast(f32x4, v);
     }
-  }
-  __syncthreads();
-  // conditioner + bias of this lane's gate / filter rows (issued before GEMM 1, used after it)
-  vec4 cnd[2][8];
-  {
-    const T* cb = (const T*)a.cond + (size_t)a.layer * a.B * N * 128;   // layer-major: one stream per layer
-#pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int n = min(n0 + p * 16 + (lane & 15), N - 1);
-      const T* cp = cb + ((size_t)b * N + n) * 128;
-      cnd[0][p] = *(const vec4*)(cp + cg);
-      cnd[1][p] = *(const vec4*)(cp + cg + 64);
-    }
-  }
+  };
+  if constexpr (ES == 2) stage_pass(0);            // straight-line: the loads above stay in flight
+  else
+    for (int u0 = 0; u0 < NUr; u0 += MAXU * 256) stage_pass(u0);
+  lds_sync();                                      // (the conditioner / residual loads stay in flight)
   // ---- 2. dilated conv GEMM: rows {16w.., 64+16w..} x 128 samples, K = 192 ----
   f32x4 acc[2][8];
 #pragma unroll
   for (int c = 0; c < 2; ++c)
 #pragma unroll
     for (int p = 0; p < 8; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const T* w1 = (const T*)a.w1;
 #pragma unroll
   for (int s = 0; s < 6; ++s) {
     const int tap = s >> 1, half = s & 1;
     Frag<T> af[2];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-      af[c] = load_frag<T>((const char*)(w1 + (size_t)(c * 64 + wave * 16 + (lane & 15)) * 192 + s * 32 + g * 8));
+    for (int c = 0; c < 2; ++c) af[c] = PRE ? aw1[PRE ? s : 0][c] : w1frag(s, c);
     const char* pb = yin + ((win ? 0 : tap * UPS) + (half * 32 + g * 8) / VE) * PL +
                      ((win ? tap * d : 0) + (lane & 15)) * 16;
 #pragma unroll
@@ -293,11 +336,8 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
     }
   }
   // ---- gated activation z = sigmoid(gate) * tanh(filter) -> LDS (plane-major, over yin) ----
-  __syncthreads();                                // every wave is done reading yin
+  lds_sync();                                      // every wave is done reading yin
   {
-    float bg[4], bfl[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) { bg[i] = a.b1[cg + i]; bfl[i] = a.b1[cg + 64 + i]; }
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       float z[4];
@@ -305,42 +345,44 @@ __global__ __launch_bounds__(256, 3) void dw_layer_kernel(DWLayerArgs a) {
       for (int i = 0; i < 4; ++i) {
         const float gate = acc[0][p][i] + bg[i] + to_f32<T>(cnd[0][p][i]);
         const float filt = acc[1][p][i] + bfl[i] + to_f32<T>(cnd[1][p][i]);
-        z[i] = dw_sigmoid(gate) * tanhf(filt);
+        z[i] = dw_sigmoid_fast(gate) * dw_tanh_fast(filt);
       }
       char* zp = zl + (cg / VE) * PLANE + (p * 16 + (lane & 15)) * 16 + (cg % VE) * ES;
       store4<T>((T*)zp, z[0], z[1], z[2], z[3]);
       const int n = n0 + p * 16 + (lane & 15);      // z of every layer, for the deferred skip GEMM
-      if (n < N) store4<T>((T*)a.z + (((size_t)a.layer * a.B + b) * N + n) * DW_C + cg, z[0], z[1], z[2], z[3]);
+      if (n0 + DW_MS <= N || n < N) store4<T>((T*)a.z + (((size_t)a.layer * a.B + b) * N + n) * DW_C + cg, z[0], z[1], z[2], z[3]);
     }
   }
-  __syncthreads();
+  lds_sync();                                      // (the z stores stay in flight)
   // ---- 3. output_residual GEMM: rows 16w.., K = 64 (output_projection is deferred: dw_skip_kernel) ----
 #pragma unroll
   for (int p = 0; p < 8; ++p) acc[0][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const T* w2 = (const T*)a.w2;
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const Frag<T> af = load_frag<T>((const char*)(w2 + (size_t)(wave * 16 + (lane & 15)) * DW_C + s * 32 + g * 8));
+    const Frag<T> af = PRE ? aw2[PRE ? s : 0] : w2frag(s);
     const char* pb = zl + ((s * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
 #pragma unroll
     for (int p = 0; p < 8; ++p) mfma_frag(acc[0][p], af, load_planes<T>(pb + p * 256, PLANE));
   }
   // ---- epilogue: x_out = (x + residual) / sqrt(2) ----
   {
-    const float r2 = 1.41421353816986083984375f;   // (float)sqrt(2.0) (diffwave.py:108)
-    float br[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) br[i] = a.b2[cg + i];
+    // (x + residual) / sqrt(2) (diffwave.py:108): the fp32 path divides like the reference; the
+    // 16-bit paths multiply by the reciprocal (<= 1 ulp of fp32 before the storage rounding)
+    const float r2 = 1.41421353816986083984375f;   // (float)sqrt(2.0)
+    const float ir2 = 0.707106769084930419921875f;  // (float)(1 / sqrt(2.0))
+    auto scale = [&](float v) { return sizeof(T) == 4 ? v / r2 : v * ir2; };
     T* xo = (T*)a.x_out + (size_t)b * N * DW_C;
+    const bool full = n0 + DW_MS <= N;              // block-uniform: no per-row checks
 #pragma unroll
     for (int p = 0; p < 8; ++p) {
       const int n = n0 + p * 16 + (lane & 15);
-      if (n >= N) continue;
-      const vec4 xv = *(const vec4*)(xin + (size_t)n * DW_C + cg);
-      store4<T>(xo + (size_t)n * DW_C + cg, (to_f32<T>(xv[0]) + (acc[0][p][0] + br[0])) / r2,
-                (to_f32<T>(xv[1]) + (acc[0][p][1] + br[1])) / r2, (to_f32<T>(xv[2]) + (acc[0][p][2] + br[2])) / r2,
-                (to_f32<T>(xv[3]) + (acc[0][p][3] + br[3])) / r2);
+      if (!full && n >= N) continue;
+      const vec4 xv = xres[p];
+      store4<T>(xo + (size_t)n * DW_C + cg, scale(to_f32<T>(xv[0]) + (acc[0][p][0] + br[0])),
+                scale(to_f32<T>(xv[1]) + (acc[0][p][1] + br[1])), scale(to_f32<T>(xv[2]) + (acc[0][p][2] + br[2])),
+                scale(to_f32<T>(xv[3]) + (acc[0][p][3] + br[3])));
     }
+  }
   }
 }
 
@@ -351,10 +393,22 @@ size_t dw_layer_lds_bytes(int dtype) {
 
 hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
   const dim3 grid((a.N + DW_MS - 1) / DW_MS, a.B);
+  {  // the staging of one block fits a single pass of 12 units per thread
+    const int ups = DW_C * (dtype == DT_F32 ? 4 : 2) / 16, pb = 64 / ups;
+    const bool win = a.dil <= 64;
+    const int rows = win ? (DW_MS + 2 * a.dil + pb - 1) / pb * pb : DW_MS;
+    if (dtype != DT_F32 && (win ? 1 : 3) * rows * ups > 12 * 256) return hipErrorInvalidValue;
+  }
   const size_t lds = dw_layer_lds_bytes(dtype);
-  if (dtype == DT_F32) hipLaunchKernelGGL(dw_layer_kernel<float>, grid, dim3(256), lds, s, a);
-  else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_layer_kernel<bf16_t>, grid, dim3(256), lds, s, a);
-  else hipLaunchKernelGGL(dw_layer_kernel<f16_t>, grid, dim3(256), lds, s, a);
+  static const bool nopre = std::getenv("SDDM_DW_NOPRE") != nullptr;   // experiment knob
+  if (dtype == DT_F32) hipLaunchKernelGGL((dw_layer_kernel<float, false>), grid, dim3(256), lds, s, a);
+  else if (dtype == DT_BF16) {
+    if (nopre) hipLaunchKernelGGL((dw_layer_kernel<bf16_t, false>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((dw_layer_kernel<bf16_t, true>), grid, dim3(256), lds, s, a);
+  } else {
+    if (nopre) hipLaunchKernelGGL((dw_layer_kernel<f16_t, false>), grid, dim3(256), lds, s, a);
+    else hipLaunchKernelGGL((dw_layer_kernel<f16_t, true>), grid, dim3(256), lds, s, a);
+  }
   return hipGetLastError();
 }
 
