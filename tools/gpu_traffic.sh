@@ -1,9 +1,13 @@
-# HBM traffic of one sampling step per kernel: FETCH_SIZE and WRITE_SIZE in separate rocprofv3
-# --pmc passes (they cannot share a pass), over tools/profile_ops.py --timesteps 1 (B=16, bf16)
+# HBM traffic per kernel launch: FETCH_SIZE and WRITE_SIZE in separate rocprofv3 --pmc passes
+# (they cannot share a pass) over tools/profile_ops.py (B=16 x 16448, bf16, 2 reverse steps);
+# tools/traffic.py maps the last step's dispatches onto the op list and writes profiles/<name>.json
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
+mkdir -p gpurun_out
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 120 rocprofv3 --pmc $c --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/traffic_$c -o run -- python3 tools/profile_ops.py --timesteps 1 > gpurun_out/traffic_$c.log 2>&1 || { echo TRAFFIC_FAIL $c; tail -5 gpurun_out/traffic_$c.log; exit 1; }
+  rm -rf gpurun_out/traffic_$c
+  timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/traffic_$c -o run -- python3 tools/profile_ops.py --timesteps 2 --json gpurun_out/traffic_ops_$c.json > gpurun_out/traffic_$c.log 2>&1 || { echo TRAFFIC_FAIL $c; tail -5 gpurun_out/traffic_$c.log; exit 1; }
 done
+python3 tools/traffic.py ${TRAFFIC_OUT:-profiles/r02_hbm_traffic.json} | cut -c1-600
 echo TRAFFIC_OK
