@@ -195,6 +195,22 @@ namespace sddm {
 #define SDDM_STAMP(args, k) do {} while (0)
 #endif
 
+// XCD-aware block order.  The logical grid (X tiles, Y images, Z channel blocks) is launched as
+// one dimension; blocks are dealt round-robin over the 8 XCDs (block id % 8 shares an L2), so
+// block id is mapped to position (id % 8) * total/8 + id / 8 of the z-major order: each XCD's
+// blocks cover one contiguous run of channel blocks (the same weight slices) and of images and
+// adjacent tiles (shared halos) and read them from its own L2 instead of each XCD fetching every
+// weight slice.  Speed only, never correctness (HIP does not promise the placement).
+__device__ __forceinline__ void xcd_block(int X, int Z, int& x, int& y, int& z) {
+  const int total = (int)gridDim.x, Y = total / (X * Z);
+  const int id = (int)blockIdx.x;
+  const int j = (total & 7) == 0 ? (id & 7) * (total >> 3) + (id >> 3) : id;
+  x = j % X;
+  const int r = j / X;
+  y = r % Y;
+  z = r / Y;
+}
+
 // floor(n / d) for 0 <= n < 2^21 from the float reciprocal rd = 1 / d: ((n + .5) * rd) is off by
 // less than the .5 / d margin, so the truncation is exact (no integer division sequence).
 __device__ __forceinline__ int fdivi(int n, float rd) { return (int)(((float)n + 0.5f) * rd); }

@@ -91,7 +91,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  const int tile = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NB;
+  int tile, b, zb;
+  xcd_block(a.n_tiles, a.Cout / NB, tile, b, zb);
+  const int n0 = zb * NB;
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int y0 = ty * a.TR, x0 = tx * a.TW;
   const int npv = a.TR * a.TW;         // valid pixels (< MT only for images smaller than a tile)
@@ -419,7 +421,7 @@ static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   if (a.TR * a.TW > MT || a.Cout % NB || (a.CA + a.CB) % 32 || (a.CA + a.CB) > 1000 || (a.RCA + a.RCB) % 32)
     return hipErrorInvalidValue;
   if (lay.total > 160 * 1024) return hipErrorInvalidValue;
-  const dim3 grid(a.n_tiles, B, a.Cout / NB), blk(64 * NW);
+  const dim3 grid(a.n_tiles * B * (a.Cout / NB)), blk(64 * NW);
   const int D = deep_ring<T, MT, NW>((nck * 9 + rck + NW - 1) / NW);
 #define SDDM_RING(DV)                                                                         \
   if (D == DV) {                                                                              \

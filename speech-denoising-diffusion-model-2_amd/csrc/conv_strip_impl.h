@@ -61,7 +61,9 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   extern __shared__ __attribute__((aligned(16))) char smem[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int strip = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NBLK;
+  int strip, b, zb;
+  xcd_block(a.n_tiles, a.Cout / NBLK, strip, b, zb);
+  const int n0 = zb * NBLK;
   const int H = a.Ho;
   const int RC = a.RCA + a.RCB;
   const int rck = RES == 2 ? RC / 32 : 0;
@@ -389,7 +391,8 @@ static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size
   if (lds > 160 * 1024 || a.Ho % SR || SR % (2 * TR) || a.Cout % (16 * FC) || a.res_mode < 0 || a.res_mode > 2 ||
       (a.res_mode == 2 && (a.RCA + a.RCB) > 128))
     return hipErrorInvalidValue;
-  const dim3 grid(a.Ho / SR, B, a.Cout / (16 * FC)), blk(MPI * 2);
+  if (a.n_tiles != a.Ho / SR) return hipErrorInvalidValue;
+  const dim3 grid((a.Ho / SR) * B * (a.Cout / (16 * FC))), blk(MPI * 2);
   if (a.res_mode == 0) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0>), grid, blk, lds, s, a, SR);
   else if (a.res_mode == 1) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 1>), grid, blk, lds, s, a, SR);
   else hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 2>), grid, blk, lds, s, a, SR);

@@ -88,7 +88,9 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c16 = lane & 15, q = lane & 3;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wp = wv % WPX, wc = wv / WPX;
-  const int tile = blockIdx.x, b = blockIdx.y, n0 = blockIdx.z * NB;
+  int tile, b, zb;
+  xcd_block(a.n_tiles, a.Cout / NB, tile, b, zb);
+  const int n0 = zb * NB;
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int y0 = ty * a.TR, x0 = tx * a.TW;
   const int npv = a.TR * a.TW;                             // valid pixels (< MT: image smaller than a tile)
@@ -388,7 +390,7 @@ static hipError_t tile_go(const ConvArgs& a, int B, hipStream_t s) {
       lds > 160 * 1024 || !a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_tile_kernel<T, S2, c.wpx, c.wco, c.fp, c.fc, S2 ? c.maxu_s2 : c.maxu>),
-                     dim3(a.n_tiles, B, a.Cout / NB), dim3(64 * c.wpx * c.wco), lds, s, a);
+                     dim3(a.n_tiles * B * (a.Cout / NB)), dim3(64 * c.wpx * c.wco), lds, s, a);
   return hipGetLastError();
 }
 
