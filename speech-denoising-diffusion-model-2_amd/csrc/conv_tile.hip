@@ -66,9 +66,10 @@ __host__ __device__ inline TileGeo tile_geo(bool s2, int TR, int TW, int MT, boo
   return g;
 }
 
-// LDS: two operand images, two weight chunks (576 B per output channel), GroupNorm scale / shift
-__host__ __device__ inline int tile_lds(const TileGeo& g, int NB, int Cin) {
-  return 2 * g.ibb + 2 * 576 * NB + 2 * Cin * 4;
+// LDS: two operand images, two weight chunks (576 B per output channel), GroupNorm scale / shift;
+// a single K chunk (nk == 1) needs one of each
+__host__ __device__ inline int tile_lds(const TileGeo& g, int NB, int Cin, int nbuf) {
+  return nbuf * g.ibb + nbuf * 576 * NB + 2 * Cin * 4;
 }
 
 __device__ __forceinline__ void glds16(const void* src, void* lds) {
@@ -100,9 +101,10 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   const bool gn = a.gamma != nullptr, ident = a.res_mode == 1;
   const TileGeo geo = tile_geo(S2, a.TR, a.TW, MT, rck > 0);
   const int HC = geo.HC, HE = geo.HE, PLB = geo.PLB;
-  char* IB = smem;                                         // [2][4 planes][PLB] operand images
-  char* WB = IB + 2 * geo.ibb;                             // [2][WCH]           weight chunks
-  float* gsc = (float*)(WB + 2 * WCH);                     // [2][Cin]           GroupNorm scale / shift
+  const int nbuf = nk > 1 ? 2 : 1;                         // double buffers only when K streams
+  char* IB = smem;                                         // [nbuf][4 planes][PLB] operand images
+  char* WB = IB + nbuf * geo.ibb;                          // [nbuf][WCH]           weight chunks
+  float* gsc = (float*)(WB + nbuf * WCH);                  // [2][Cin]              GroupNorm scale / shift
   const float rHC = 1.0f / (float)HC, rTW = 1.0f / (float)a.TW;
   const int img_in = a.Hi * a.Wi, img_out = a.Ho * a.Wo;
   const T* srcA = (const T*)a.srcA + (size_t)b * img_in * a.CA;
@@ -378,7 +380,8 @@ static size_t tile_lds_cfg(bool s2, const ConvArgs& a) {
   const TileGeo g = tile_geo(s2, a.TR, a.TW, MT, a.res_mode == 2);
   const int NT = 64 * c.wpx * c.wco, maxu = s2 ? c.maxu_s2 : c.maxu;
   if (g.nu3 > maxu * NT || g.nur > maxu * NT) return (size_t)1 << 40;   // more staging units than registers
-  return (size_t)tile_lds(g, NB, a.CA + a.CB);
+  const int nk = (a.CA + a.CB) / 32 + (a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0);
+  return (size_t)tile_lds(g, NB, a.CA + a.CB, nk > 1 ? 2 : 1);
 }
 
 template <typename T, bool S2, int I>
