@@ -6,6 +6,8 @@
 // lane group are consumed by 8 MFMA 16x16x4 instructions (element j -> k-set {j, 8+j, 16+j,
 // 24+j}); any k permutation shared by A and B gives the same dot product.
 #pragma once
+#include <cstdlib>
+
 #include "sddm_common.h"
 
 namespace sddm {
@@ -202,6 +204,10 @@ namespace sddm {
 // adjacent tiles (shared halos) and read them from its own L2 instead of each XCD fetching every
 // weight slice.  Speed only, never correctness (HIP does not promise the placement).
 __device__ __forceinline__ void xcd_block(int X, int Z, int& x, int& y, int& z) {
+  if (gridDim.y > 1 || gridDim.z > 1) {             // launched in plain (x, y, z) order
+    x = blockIdx.x; y = blockIdx.y; z = blockIdx.z;
+    return;
+  }
   const int total = (int)gridDim.x, Y = total / (X * Z);
   const int id = (int)blockIdx.x;
   const int j = (total & 7) == 0 ? (id & 7) * (total >> 3) + (id >> 3) : id;
@@ -209,6 +215,12 @@ __device__ __forceinline__ void xcd_block(int X, int Z, int& x, int& y, int& z) 
   const int r = j / X;
   y = r % Y;
   z = r / Y;
+}
+
+// host: the launch grid for xcd_block (SDDM_XCD=0 selects the plain order, for A/B runs)
+__host__ inline dim3 xcd_grid(int X, int Y, int Z) {
+  static const bool plain = std::getenv("SDDM_XCD") && std::atoi(std::getenv("SDDM_XCD")) == 0;
+  return plain ? dim3(X, Y, Z) : dim3(X * Y * Z);
 }
 
 // floor(n / d) for 0 <= n < 2^21 from the float reciprocal rd = 1 / d: ((n + .5) * rd) is off by

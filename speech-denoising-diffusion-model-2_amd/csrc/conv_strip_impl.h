@@ -392,7 +392,7 @@ static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size
       (a.res_mode == 2 && (a.RCA + a.RCB) > 128))
     return hipErrorInvalidValue;
   if (a.n_tiles != a.Ho / SR) return hipErrorInvalidValue;
-  const dim3 grid((a.Ho / SR) * B * (a.Cout / (16 * FC))), blk(MPI * 2);
+  const dim3 grid = xcd_grid(a.Ho / SR, B, a.Cout / (16 * FC)), blk(MPI * 2);
   if (a.res_mode == 0) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0>), grid, blk, lds, s, a, SR);
   else if (a.res_mode == 1) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 1>), grid, blk, lds, s, a, SR);
   else hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 2>), grid, blk, lds, s, a, SR);

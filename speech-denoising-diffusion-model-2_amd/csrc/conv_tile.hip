@@ -393,7 +393,7 @@ static hipError_t tile_go(const ConvArgs& a, int B, hipStream_t s) {
       lds > 160 * 1024 || !a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_tile_kernel<T, S2, c.wpx, c.wco, c.fp, c.fc, S2 ? c.maxu_s2 : c.maxu>),
-                     dim3(a.n_tiles * B * (a.Cout / NB)), dim3(64 * c.wpx * c.wco), lds, s, a);
+                     xcd_grid(a.n_tiles, B, a.Cout / NB), dim3(64 * c.wpx * c.wco), lds, s, a);
   return hipGetLastError();
 }
 

@@ -216,7 +216,7 @@ hipError_t launch_dw_input(int dtype, const DWInArgs& a, hipStream_t s) {
 // PREW: the 16-bit weight fragments held in registers for the whole block (236 VGPRs: two blocks
 // per CU); without, loaded per K step (three blocks per CU)
 template <typename T, bool PREW>
-__global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs a) {
+__global__ __launch_bounds__(256, (PREW || sizeof(T) == 4) ? 2 : 3) void dw_layer_kernel(DWLayerArgs a) {
   constexpr int ES = (int)sizeof(T), VE = 16 / ES;
   constexpr int UPS = DW_C / VE;                  // 16-byte units (planes) per sample and tap
   constexpr int PB = 64 / UPS;                    // samples per 64-unit staging group
@@ -226,6 +226,8 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* yin = smem;                               // [3 taps][UPS][128 samples][16 B]
   char* zl = smem;                                // [UPS][128 samples][16 B], aliases yin after GEMM 1
+  constexpr int XS = DW_C * ES + 16;              // residual row stride (16-byte aligned, staggers banks)
+  char* xl = smem + 3 * UPS * PLANE;              // [128 samples][XS]: raw x of the tile (residual)
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -254,6 +256,8 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
   for (int i = 0; i < 4; ++i) { bg[i] = a.b1[cg + i]; bfl[i] = a.b1[cg + 64 + i]; br[i] = a.b2[cg + i]; }
   const int t_now = a.t_dev ? *a.t_dev : 0;
   {
+  // plain order: round-robin dealing spreads a clip's neighbouring tiles over the XCDs (measured
+  // faster than the XCD-contiguous order of the conv kernels: 216.6 vs 228.6 us per layer)
   const int b = blockIdx.y, n0 = blockIdx.x * DW_MS;
   const T* xin = (const T*)a.x_in + (size_t)b * N * DW_C;
   const float* ds = a.ds + ((size_t)(a.ds_per_b ? b : t_now) * a.L + a.layer) * DW_C;
@@ -267,7 +271,7 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
   // then every other load that does not depend on the staged image, so a tile waits on memory
   // once: the conditioner rows of this lane's gate / filter channels (used after GEMM 1) and the
   // residual x of its output channels (used in the epilogue); clamped, unconditional
-  vec4 cnd[2][8], xres[8];
+  vec4 cnd[2][8];
   {
     const T* cb = (const T*)a.cond + (size_t)a.layer * a.B * N * 128;   // layer-major: one stream per layer
 #pragma unroll
@@ -276,7 +280,6 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
       const T* cp = cb + ((size_t)b * N + n) * 128;
       cnd[0][p] = *(const vec4*)(cp + cg);
       cnd[1][p] = *(const vec4*)(cp + cg + 64);
-      xres[p] = *(const vec4*)(xin + (size_t)n * DW_C + cg);
     }
   }
   // ---- 1. y = x + diffusion projection -> LDS ----
@@ -289,7 +292,7 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
   const int NUr = TAPS * ROWS * UPS;             // 16-bit: <= MAXU * 256 (checked by the launcher)
   auto stage_pass = [&](int u0) {
     f32x4 reg[MAXU];
-    int dst[MAXU], qv[MAXU];
+    int dst[MAXU], qv[MAXU], xr[MAXU];
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       const int u = min(u0 + tid + k * 256, NUr - 1);
@@ -300,10 +303,14 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
       reg[k] = *(const f32x4*)(xin + (size_t)min(max(n, 0), N - 1) * DW_C + q * VE);
       dst[k] = (u0 + tid + k * 256 < NUr) ? ((tap * UPS + q) * PL + s * 16) : -1;
       qv[k] = ok ? 1 : 0;
+      // the centre rows n0 .. n0+127 also go to the residual image, raw
+      const int c = n - n0;
+      xr[k] = (u0 + tid + k * 256 < NUr && (win || tap == 1) && c >= 0 && c < DW_MS) ? c * XS + q * 16 : -1;
     }
 #pragma unroll
     for (int k = 0; k < MAXU; ++k) {
       typedef T vec __attribute__((ext_vector_type(VE)));
+      if (xr[k] >= 0) *(f32x4*)(xl + xr[k]) = reg[k];
       vec v = __builtin_bit_cast(vec, reg[k]);
 #pragma unroll
       for (int e = 0; e < VE; ++e) v[e] = from_f32<T>(qv[k] ? to_f32<T>(v[e]) + dsv[e] : 0.f);
@@ -377,7 +384,7 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
     for (int p = 0; p < 8; ++p) {
       const int n = n0 + p * 16 + (lane & 15);
       if (!full && n >= N) continue;
-      const vec4 xv = xres[p];
+      const vec4 xv = *(const vec4*)(xl + (p * 16 + (lane & 15)) * XS + cg * ES);
       store4<T>(xo + (size_t)n * DW_C + cg, scale(to_f32<T>(xv[0]) + (acc[0][p][0] + br[0])),
                 scale(to_f32<T>(xv[1]) + (acc[0][p][1] + br[1])), scale(to_f32<T>(xv[2]) + (acc[0][p][2] + br[2])),
                 scale(to_f32<T>(xv[3]) + (acc[0][p][3] + br[3])));
@@ -387,8 +394,8 @@ __global__ __launch_bounds__(256, PREW ? 2 : 3) void dw_layer_kernel(DWLayerArgs
 }
 
 size_t dw_layer_lds_bytes(int dtype) {
-  const int ups = DW_C * (dtype == DT_F32 ? 4 : 2) / 16;
-  return (size_t)3 * ups * DW_MS * 16;
+  const int es = dtype == DT_F32 ? 4 : 2, ups = DW_C * es / 16;
+  return (size_t)3 * ups * DW_MS * 16 + (size_t)DW_MS * (DW_C * es + 16);   // staging + residual rows
 }
 
 hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
