@@ -70,8 +70,25 @@ class SDDM(nn.Module):
             self._ctx, self._ctx_key = ctx, key
         return self._ctx
 
-    def forward(self, target, condition):
-        raise NotImplementedError("SDDM.forward is the training step (model.py:29-48), outside the sampling hot path")
+    @torch.no_grad()
+    def forward(self, target, condition, noise=None, t=None, random_step=None):
+        """Training-step forward (model.py:29-48): q-sample x_t from the target, estimate its noise.
+        Returns (predicted, noise) like the reference.  Both pieces run on HIP (sddm_q_sample, then
+        the network forward); the draws (randn_like / randint / rand on the target's device) are the
+        reference's unless given.  Inference-only: the HIP path has no backward, so no autograd."""
+        if not target.is_cuda:
+            raise RuntimeError("SDDM.forward runs on the HIP device; move the tensors to cuda")
+        if noise is None:
+            noise = torch.randn_like(target, device=target.device)
+        net = self.noise_estimate_model
+        if self.q_transition == "original":
+            x_t, noise_level, steps = self.diffusion.q_stochastic(target, noise, t=t, random_step=random_step)
+            level = noise_level if self.noise_condition == "sqrt_alpha_bar" else steps
+            predicted = net(condition, x_t, level)
+        else:
+            x_t, noise, noise_level = self.diffusion.q_stochastic_conditional(target, condition, noise, t=t)
+            predicted = net(condition, x_t, noise_level)
+        return predicted, noise
 
     @torch.no_grad()
     def infer(self, condition, continuous=False, seed=None, row_offset=0):

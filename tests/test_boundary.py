@@ -96,6 +96,15 @@ def test_facade_rejects_unknown_modes_like_reference():
         M.SDDM(D.GaussianDiffusion("linear", 10, device="cpu"), torch.nn.Identity(), noise_condition="snr")
 
 
+def test_training_forward_needs_the_hip_device():
+    """SDDM.forward (model.py:29-48) runs q-sample + network on HIP; host tensors raise, never a
+    silent CPU fallback."""
+    m = _build()
+    x = torch.zeros(1, 1, 2112)
+    with pytest.raises(RuntimeError):
+        m(x, x)
+
+
 def test_facade_geometry_assert_like_reference():
     import model.network as NW
     with pytest.raises(AssertionError):

@@ -98,3 +98,47 @@ def test_bf16_sampling_close_to_fp32(torch_cuda):
     err = rms(out, inf[key + "/out"])
     print("bf16 50-step rms vs fp32 reference", err)
     assert err <= 1e-2     # bf16 network storage: stated tolerance
+
+
+@pytest.mark.parametrize("q_transition,noise_condition", [("original", "sqrt_alpha_bar"), ("original", "time_step"),
+                                                          ("conditional", "sqrt_alpha_bar")])
+def test_sddm_forward_training_step(torch_cuda, q_transition, noise_condition):
+    """SDDM.forward (model.py:29-48): q-sample on HIP, then the network on HIP, against the oracle's
+    q_stochastic* (diffusion.py:225-279, pinned by q_sample.npz) composed with oracle/unet.forward
+    (pinned by unet_forward.npz), with the reference's draws (randint / rand) made explicit."""
+    import model.diffusion as D
+    import model.model as M
+    import model.network as NW
+    from oracle import sampler as osamp, unet as ounet
+    from oracle.schedule import BUFFER_NAMES
+    from _helpers import unet_arch
+    from sddm_hip.synth import noisy_speech
+    N, B, T = 2112, 3, 100
+    dev = torch.device("cuda", 0)
+    d = D.GaussianDiffusion("linear", T, 1e-6, 1e-3, device=dev)
+    n = NW.UNetModified2(num_samples=N, **UNET_NET["args"])
+    P = unet_params(N)
+    n.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    m = M.SDDM(d, n, noise_condition=noise_condition, q_transition=q_transition).to(dev)
+    target = noisy_speech(B, N, seed=11)
+    cond = noisy_speech(B, N, seed=12)
+    rng = np.random.default_rng(3)
+    noise = rng.standard_normal(target.shape).astype(np.float32)
+    t = np.array([1, 37, T], dtype=np.int64)
+    r = rng.random(B).astype(np.float32)
+    tab = {k: getattr(d, k).cpu().numpy() for k in BUFFER_NAMES}
+    tg = lambda a: torch.from_numpy(a).to(dev)
+    if q_transition == "original":
+        pred, nz = m(tg(target), tg(cond), noise=tg(noise), t=tg(t), random_step=tg(r))
+        x_t, s, level = osamp.q_stochastic(tab, target, noise, t, r)
+        nl = s if noise_condition == "sqrt_alpha_bar" else level
+        ref_noise = noise
+    else:
+        pred, nz = m(tg(target), tg(cond), noise=tg(noise), t=tg(t.reshape(B, 1, 1)))
+        x_t, ref_noise, nl = osamp.q_stochastic_conditional(tab, target, cond, noise, t)
+    ref = ounet.forward(P, unet_arch(N), cond, x_t, np.asarray(nl, np.float32).reshape(-1))
+    assert pred.shape == (B, 1, N) and nz.shape == (B, 1, N)
+    assert np.abs(nz.cpu().numpy() - ref_noise).max() <= 1e-5
+    assert rms(pred.cpu().numpy(), ref) <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))))
+    with pytest.raises(RuntimeError):
+        m(tg(target).cpu(), tg(cond).cpu())
