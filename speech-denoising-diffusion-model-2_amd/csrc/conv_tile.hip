@@ -47,6 +47,7 @@ static constexpr TileCfgX kTileCfgs[] = {
     {1, 1, 2, 1, 4, 10},   //  9:  32 px x 16 co, 1 wave
     {4, 2, 2, 3, 3, 6},    // 10: 128 px x 96 co, 8 waves
     {2, 1, 2, 2, 4, 10},   // 11:  64 px x 32 co, 2 waves
+    {8, 1, 4, 2, 6, 10},   // 12: 512 px x 32 co, 8 waves (the 128 x 64 level in one round of blocks; stride 1)
 };
 static constexpr int kNTileCfgs = (int)(sizeof(kTileCfgs) / sizeof(kTileCfgs[0]));
 
@@ -403,7 +404,7 @@ static hipError_t tile_dispatch(int cfg, const ConvArgs& a, int B, hipStream_t s
 #define SDDM_TILE(I) \
   case I: return tile_go<T, S2, I>(a, B, s);
     SDDM_TILE(0) SDDM_TILE(1) SDDM_TILE(2) SDDM_TILE(3) SDDM_TILE(4) SDDM_TILE(5)
-    SDDM_TILE(6) SDDM_TILE(7) SDDM_TILE(8) SDDM_TILE(9) SDDM_TILE(10) SDDM_TILE(11)
+    SDDM_TILE(6) SDDM_TILE(7) SDDM_TILE(8) SDDM_TILE(9) SDDM_TILE(10) SDDM_TILE(11) SDDM_TILE(12)
 #undef SDDM_TILE
     default: return hipErrorInvalidValue;
   }
@@ -426,7 +427,7 @@ size_t conv_tile_lds_bytes(int cfg, bool s2, const ConvArgs& a) {
 #define SDDM_TILE(I) \
   case I: return tile_lds_cfg<I>(s2, a);
     SDDM_TILE(0) SDDM_TILE(1) SDDM_TILE(2) SDDM_TILE(3) SDDM_TILE(4) SDDM_TILE(5)
-    SDDM_TILE(6) SDDM_TILE(7) SDDM_TILE(8) SDDM_TILE(9) SDDM_TILE(10) SDDM_TILE(11)
+    SDDM_TILE(6) SDDM_TILE(7) SDDM_TILE(8) SDDM_TILE(9) SDDM_TILE(10) SDDM_TILE(11) SDDM_TILE(12)
 #undef SDDM_TILE
     default: return (size_t)1 << 40;
   }

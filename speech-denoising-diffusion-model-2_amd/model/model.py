@@ -18,7 +18,8 @@ from torch import nn
 import sddm_hip
 from .diffusion import GaussianDiffusion, _seed_from_torch
 
-_TUNING = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "conv_tuning.json")
+_TUNING = os.environ.get("SDDM_TUNING_FILE") or os.path.join(
+    os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "configs", "conv_tuning.json")
 _P_TRANSITIONS = ("original", "supportive", "sr3", "conditional", "condition_in")
 
 

@@ -83,12 +83,12 @@ def bench_rows(N=16448, B=16):
 
 
 # per-layer kernel table exercising every kernel family on the bench geometry (tile configurations
-# of 1, 2, 4, 6 and 8 waves, stride 2, upsample, virtual concat, res_conv chunks, conv_deep tiles)
+# of 1, 2, 4, 6 and 8 waves, the 512-pixel tile, stride 2, upsample, virtual concat, res_conv chunks, conv_deep tiles)
 _TUNING = {"downs.4": "tile:2", "downs.5.block1": "tile:10", "downs.5.block2": "tile:6", "downs.6": "tile:4",
            "downs.7.block1": "tile:8", "downs.8": "tile:7", "downs.9.block2": "deep:32:8", "downs.10": "tile:9",
            "mid.0.block1": "tile:8", "mid.0.block2": "deep", "ups.0.block1": "tile:9", "ups.4": "tile:6",
            "ups.5.block1": "tile:11", "ups.7": "tile:3", "ups.8.block1": "tile:1", "ups.8.block2": "tile:0",
-           "ups.11.block1": "tile:1", "ups.12.block1": "strip"}
+           "ups.11.block1": "tile:1", "ups.12.block1": "strip", "downs.3.block2": "tile:12"}
 
 
 # conv_deep with 16-channel blocks: every pixel tile (16..128), both wave counts, stride 2,
