@@ -243,6 +243,7 @@ def test_multilane_graph_replay_equals_row_blocks(torch_cuda, monkeypatch):
     from sddm_hip.synth import noisy_speech
     N, B, sched = 2112, 40, ("linear", 6, 1e-6, 1e-3)
     cond = noisy_speech(B, N, seed=77)
+    monkeypatch.setenv("SDDM_LANE_ROWS", "16")
     ctx = make_ctx(N, "bfloat16", sched)
     full = _sample(torch_cuda, ctx, cond)
     blocks = np.concatenate([_sample(torch_cuda, ctx, cond[r:r + 16], row_offset=r) for r in (0, 16, 32)])
@@ -251,6 +252,11 @@ def test_multilane_graph_replay_equals_row_blocks(torch_cuda, monkeypatch):
     monkeypatch.setenv("SDDM_NO_GRAPH", "1")
     assert np.array_equal(_sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond), full)
     monkeypatch.delenv("SDDM_NO_GRAPH")
+    monkeypatch.delenv("SDDM_LANE_ROWS")
+    full64 = _sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond)   # default: one 40-row lane
+    assert np.array_equal(full64, _sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond))
+    print(f"one 40-row lane vs 16-row lanes: rms {rms(full64, full):.3e}")
+    assert rms(full64, full) <= 1e-2
     monkeypatch.setenv("SDDM_LANE_ROWS", "4")
     ctx4 = make_ctx(N, "bfloat16", sched)
     full4 = _sample(torch_cuda, ctx4, cond)
@@ -275,4 +281,23 @@ def test_headline_bf16_vs_fp32_1000_steps(torch_cuda):
     err = rms(out16, out32)
     rows = [rms(out16[b], out32[b]) for b in range(B)]
     print(f"T=1000 B=16 bf16 vs fp32: rms {err:.3e}, worst row {max(rows):.3e}, signal rms {rms(out32, 0):.3f}")
+    assert err <= 5e-3
+
+
+def test_config5_sampling_b128_lanes(torch_cuda):
+    """BASELINE config #5 per-GPU plan: B=128 chunks of 32832 samples in fp16 = 2 lanes of 64 rows
+    (the default lane size) graph-replayed on 2 streams.  A 3-step sampling run equals separate
+    64-row runs of its two row blocks (row_offset keyed noise) bit for bit, and stays within the
+    fp16 sampling tolerance of the fp32 path (fp32 itself pinned to the reference goldens)."""
+    from sddm_hip.synth import noisy_speech
+    N, B, sched = 32832, 128, ("linear", 3, 1e-6, 1e-3)
+    cond = noisy_speech(B, N, seed=55)
+    ctx = make_ctx(N, "float16", sched)
+    full = _sample(torch_cuda, ctx, cond)
+    assert np.isfinite(full).all()
+    for r in (0, 64):
+        assert np.array_equal(full[r:r + 64], _sample(torch_cuda, ctx, cond[r:r + 64], row_offset=r))
+    ref = _sample(torch_cuda, make_ctx(N, "float32", sched), cond[112:128], row_offset=112)
+    err = rms(full[112:128], ref)
+    print(f"config #5 B=128 fp16 vs fp32 (rows 112..127, 3 steps): rms {err:.3e}")
     assert err <= 5e-3
