@@ -342,6 +342,7 @@ def main():
     network = config.init_obj("network", module_network, num_samples=N)
     model = config.init_obj("arch", module_arch, diffusion, network).to(dev).eval()
     model.compute_dtype = {"bf16": "bfloat16", "f16": "float16", "f32": "float32"}[args.dtype]
+    model.lane_rows = 64 if B >= 64 else None                      # 64-row lanes for large per-GPU batches
 
     cond_all = torch.from_numpy(noisy_speech(B * world, N, seed=1234)).to(dev)   # VoiceBank-DEMAND-shaped chunks
     result = {}
@@ -399,7 +400,7 @@ def main():
                 "config": {"workload": f"UNetModified2 config_unet.json, linear 1e-6..1e-3, T={T}, "
                                        f"{B}x{N}-sample chunks per GPU, condition_in",
                            "model": "UNetModified2", "global_batch": B * world, "seq_len": N,
-                           "timesteps": T, "parallelism": f"dp{world}"},
+                           "timesteps": T, "parallelism": f"dp{world}", "lane_rows": model.lane_rows or 16},
                 "roofline": roofline, "cpu_baseline": cpu}
         print(json.dumps(line), flush=True)
     if world > 1:

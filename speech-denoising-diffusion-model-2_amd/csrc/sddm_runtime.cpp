@@ -270,7 +270,7 @@ struct sddm_ctx {
   // kStreams streams (the deep UNet levels are latency-bound: independent lanes fill the chip)
   std::vector<std::unique_ptr<Lane>> lanes;
   int plan_B = -1;
-  int lane_rows = 64;
+  int lane_rows = 16;
   int plan_gen = 0;
   hipStream_t work[kStreams] = {};
   hipEvent_t ev_in = nullptr;
@@ -1080,11 +1080,13 @@ int sddm_configure(sddm_ctx* c, const char* json) {
   const Json& diff = cfg.at("diffusion");
   const Json& net = cfg.at("network");
   c->arch_type = arch.string("type", "SDDM");
-  // rows per lane ("lane_rows", default 64; SDDM_LANE_ROWS overrides): larger lanes give the
-  // latency-bound deep levels bigger grids (config #5, B=128 per GPU: lanes of 64 sample 1.2x
-  // faster than lanes of 16)
+  // rows per lane ("lane_rows", default 16; SDDM_LANE_ROWS overrides).  Every lane's kernels are
+  // chosen for lane_rows rows, so any row partition samples bit-identically; larger lanes give the
+  // latency-bound deep levels bigger grids for large per-GPU batches (config #5, B=128 per GPU:
+  // lanes of 64 sample 1.18x faster than lanes of 16) but grids sized for 64 rows underfill a
+  // 16-row batch (the config #2 headline ran 0.62x as fast on them)
   if (!std::getenv("SDDM_LANE_ROWS")) {
-    const int lr = (int)cfg.number("lane_rows", 64);
+    const int lr = (int)cfg.number("lane_rows", 16);
     if (lr < 1) FAIL(SDDM_ERR_INVALID_ARG, "lane_rows %d", lr);
     c->lane_rows = lr;
     c->plan_B = -1;

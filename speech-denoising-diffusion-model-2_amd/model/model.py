@@ -9,6 +9,8 @@ returns x_0.  Extra keyword arguments (all optional, defaults keep the reference
   row_offset  global index of this batch's first row (multi-GPU sharding: rows keep the
               same noise whatever rank samples them)
   compute_dtype (constructor / attribute): 'float32' (parity, default), 'bfloat16', 'float16'
+  lane_rows   (attribute): rows per lane of the UNet plan (library default 16; 64 for per-GPU
+              batches of 64+ rows, e.g. config #5)
 """
 import os
 
@@ -41,6 +43,7 @@ class SDDM(nn.Module):
         if q_transition not in ("original", "conditional"):
             raise NotImplementedError
         self.compute_dtype = compute_dtype
+        self.lane_rows = None
         self._ctx = None
         self._ctx_key = None
 
@@ -50,10 +53,13 @@ class SDDM(nn.Module):
                 "q_transition": self.q_transition}
         if hasattr(self, "hop_samples"):
             args = {"noise_condition": self.noise_condition, "hop_samples": self.hop_samples}
-        return {"arch": {"type": type(self).__name__, "args": args},
-                "diffusion": {"type": "GaussianDiffusion", "args": self.diffusion.schedule_args},
-                "network": {"type": type(net).__name__, "args": net.config_args},
-                "num_samples": getattr(net, "num_samples", -1)}
+        cfg = {"arch": {"type": type(self).__name__, "args": args},
+               "diffusion": {"type": "GaussianDiffusion", "args": self.diffusion.schedule_args},
+               "network": {"type": type(net).__name__, "args": net.config_args},
+               "num_samples": getattr(net, "num_samples", -1)}
+        if getattr(self, "lane_rows", None):
+            cfg["lane_rows"] = int(self.lane_rows)
+        return cfg
 
     def _context(self, device):
         sd = dict(self.state_dict())
@@ -61,7 +67,7 @@ class SDDM(nn.Module):
         if hasattr(net, "library_params"):       # plain attributes the library needs (DiffWave)
             for k, v in net.library_params().items():
                 sd.setdefault("noise_estimate_model." + k, v)
-        key = (device.index or 0, self.compute_dtype) + tuple((k, v.data_ptr(), v._version) for k, v in sd.items())
+        key = (device.index or 0, self.compute_dtype, getattr(self, "lane_rows", None)) + tuple((k, v.data_ptr(), v._version) for k, v in sd.items())
         if self._ctx is None or self._ctx_key != key:
             ctx = sddm_hip.Context(self.library_config(), device.index or 0, self.compute_dtype)
             ctx.load_state_dict(sd)

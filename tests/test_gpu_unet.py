@@ -252,8 +252,8 @@ def test_multilane_graph_replay_equals_row_blocks(torch_cuda, monkeypatch):
     monkeypatch.setenv("SDDM_NO_GRAPH", "1")
     assert np.array_equal(_sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond), full)
     monkeypatch.delenv("SDDM_NO_GRAPH")
-    monkeypatch.delenv("SDDM_LANE_ROWS")
-    full64 = _sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond)   # default: one 40-row lane
+    monkeypatch.setenv("SDDM_LANE_ROWS", "64")
+    full64 = _sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond)   # one 40-row lane
     assert np.array_equal(full64, _sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond))
     print(f"one 40-row lane vs 16-row lanes: rms {rms(full64, full):.3e}")
     assert rms(full64, full) <= 1e-2
@@ -286,13 +286,17 @@ def test_headline_bf16_vs_fp32_1000_steps(torch_cuda):
 
 def test_config5_sampling_b128_lanes(torch_cuda):
     """BASELINE config #5 per-GPU plan: B=128 chunks of 32832 samples in fp16 = 2 lanes of 64 rows
-    (the default lane size) graph-replayed on 2 streams.  A 3-step sampling run equals separate
+    (lane_rows = 64, as bench.py sets it for per-GPU batches of 64+) graph-replayed on 2 streams.  A 3-step sampling run equals separate
     64-row runs of its two row blocks (row_offset keyed noise) bit for bit, and stays within the
     fp16 sampling tolerance of the fp32 path (fp32 itself pinned to the reference goldens)."""
     from sddm_hip.synth import noisy_speech
     N, B, sched = 32832, 128, ("linear", 3, 1e-6, 1e-3)
     cond = noisy_speech(B, N, seed=55)
-    ctx = make_ctx(N, "float16", sched)
+    cfg = unet_config(N, sched)
+    cfg["lane_rows"] = 64
+    ctx = sddm_hip.Context(cfg, 0, "float16")
+    for k, v in unet_params(N).items():
+        ctx.load_param("noise_estimate_model." + k, v)
     full = _sample(torch_cuda, ctx, cond)
     assert np.isfinite(full).all()
     for r in (0, 64):
