@@ -35,7 +35,7 @@
 
 namespace sddm {
 
-template <typename T, int FC, int W, int CIN, int MPI, int RES>
+template <typename T, int FC, int W, int CIN, int MPI, int RES, bool GN>
 __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR) {
   constexpr int NT = MPI * 2;                     // threads: one wave per 32 pixels of an iteration
   constexpr int NWV = NT / 64;
@@ -67,7 +67,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   const int H = a.Ho;
   const int RC = a.RCA + a.RCB;
   const int rck = RES == 2 ? RC / 32 : 0;
-  const bool gn = a.gamma != nullptr;
+  constexpr bool gn = GN;                         // GroupNorm + SiLU on the input (a Block conv)
 
   char* ring = smem;                              // [R][UPP planes][PL]
   char* wl = ring + R * SLOT;                     // [WPLANES][NBLK][16 B]
@@ -193,17 +193,21 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     }
   };
   // ring slots of row group j (group iters, past the strip, lands in slots nobody reads again)
-  auto commit_rows = [&](const f32x4 (&src)[UPT], int j) {
+  // unit k of row group j, transformed (branch-free: rows past the image are zeroed by a select,
+  // so the transform stays in the iteration's basic block, interleaved with the MFMAs)
+  auto xform_unit = [&](const f32x4 (&src)[UPT], int j, int k) {
+    const int ry = y0 + j * TR + 1 + pr[k];
+    f32x4 v = src[k];
+    if constexpr (GN) v = transform_lds<T>(v, gsc + cq[k], gsc + CIN + cq[k]);
+    return ry >= H ? f32x4{0.f, 0.f, 0.f, 0.f} : v;
+  };
+  auto store_rows = [&](const f32x4 (&tv)[UPT], int j) {
     const int sb = (base + j * TR + 2) % R;             // uniform
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
-      const int ry = y0 + j * TR + 1 + pr[k];
-      f32x4 v = src[k];
-      if (ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
-      else if (gn) v = transform_lds<T>(v, gsc + cq[k], gsc + CIN + cq[k]);
       int sl = sb + pr[k];
       sl = sl >= R ? sl - R : sl;
-      *(f32x4*)(ring + (int)__umul24(sl, SLOT) + loff[k]) = v;
+      *(f32x4*)(ring + (int)__umul24(sl, SLOT) + loff[k]) = tv[k];
     }
   };
   T* outb = (T*)a.out + (size_t)b * H * W * a.Cout;
@@ -276,6 +280,9 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         sl = sl >= R ? sl - R : sl;
         bptr[fp][dy] = ring + (int)__umul24(sl, SLOT) + g * UPL * PL + pcol[fp] * 16;
       }
+    // the ring refill of row group it + 1 (its rows were issued an iteration ago) is transformed
+    // between the taps' MFMAs, unit k after tap k * 9 NCK / UPT, and stored after the epilogue
+    f32x4 tv[UPT];
 #pragma unroll
     for (int ck = 0; ck < NCK; ++ck) {
 #pragma unroll
@@ -290,6 +297,9 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 #pragma unroll
           for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
         }
+#pragma unroll
+        for (int k = 0; k < UPT; ++k)
+          if (ck * 9 + tap == k * 9 * NCK / UPT) tv[k] = xform_unit(fill, it + 1, k);   // compile-time
       }
     }
     if constexpr (RES == 2) {  // ResnetBlock.res_conv 1x1 on the raw block input (fragments prefetched)
@@ -324,7 +334,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         s2[fc][1] = __builtin_elementwise_fma(d1, d1, s2[fc][1]);
       }
     }
-    commit_rows(fill, it + 1);
+    store_rows(tv, it + 1);
     lds_sync();                                          // LDS only: the prefetches stay in flight
   };
   issue_rows(rowsA, 1);
@@ -393,9 +403,11 @@ static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size
     return hipErrorInvalidValue;
   if (a.n_tiles != a.Ho / SR) return hipErrorInvalidValue;
   const dim3 grid = xcd_grid(a.Ho / SR, B, a.Cout / (16 * FC)), blk(MPI * 2);
-  if (a.res_mode == 0) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0>), grid, blk, lds, s, a, SR);
-  else if (a.res_mode == 1) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 1>), grid, blk, lds, s, a, SR);
-  else hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 2>), grid, blk, lds, s, a, SR);
+  if (a.res_mode != 0 && !a.gamma) return hipErrorInvalidValue;   // residual modes are ResnetBlock convs
+  if (a.res_mode == 0 && !a.gamma) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0, false>), grid, blk, lds, s, a, SR);
+  else if (a.res_mode == 0) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0, true>), grid, blk, lds, s, a, SR);
+  else if (a.res_mode == 1) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 1, true>), grid, blk, lds, s, a, SR);
+  else hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 2, true>), grid, blk, lds, s, a, SR);
   return hipGetLastError();
 }
 
