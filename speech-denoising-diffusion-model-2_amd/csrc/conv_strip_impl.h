@@ -30,6 +30,8 @@
 // straight-line code, so the compiler's memory-counter waits are exact, and the iteration barrier
 // orders LDS only: no iteration waits for the loads it issued.
 #pragma once
+#include <type_traits>
+
 #include "conv_common.h"
 #include "kernels.h"
 
@@ -256,13 +258,17 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   f32x4 rowsA[UPT], rowsB[UPT];
   vec4 r1A[FP][FC], r1B[FP][FC];
   Frag<T> r2A[RCKM][FP], r2B[RCKM][FP];
-  auto body = [&](int it, f32x4 (&nxt)[UPT], f32x4 (&fill)[UPT], vec4 (&r1cur)[FP][FC], vec4 (&r1nxt)[FP][FC],
-                  Frag<T> (&r2cur)[RCKM][FP], Frag<T> (&r2nxt)[RCKM][FP]) {
+  // LR / LX (compile-time): issue the rows of row group it + 2 / the residual inputs of iteration
+  // it + 1 and refill the ring; the last two iterations of a strip issue no rows and the last
+  // neither residual inputs nor a refill (the groups past the strip end were once loaded clamped
+  // and never read: up to 2x the input bytes of the 2-iteration level-1 strips)
+  auto body = [&](auto LR, auto LX, int it, f32x4 (&nxt)[UPT], f32x4 (&fill)[UPT], vec4 (&r1cur)[FP][FC],
+                  vec4 (&r1nxt)[FP][FC], Frag<T> (&r2cur)[RCKM][FP], Frag<T> (&r2nxt)[RCKM][FP]) {
     const int y = y0 + it * TR;
     const int s_it = (base + it * TR) % R;               // slot of row y - 1
-    issue_rows(nxt, it + 2);
-    if constexpr (RES == 1) issue_res1(r1nxt, it + 1);
-    if constexpr (RES == 2) issue_res2(r2nxt, it + 1);
+    if constexpr (decltype(LR)::value) issue_rows(nxt, it + 2);
+    if constexpr (RES == 1 && decltype(LX)::value) issue_res1(r1nxt, it + 1);
+    if constexpr (RES == 2 && decltype(LX)::value) issue_res2(r2nxt, it + 1);
     // keep these loads at the top of the body: the scheduler would otherwise sink them below the
     // MFMAs (shorter live ranges) and halve the prefetch distance
     __builtin_amdgcn_sched_barrier(0);
@@ -298,8 +304,8 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
           for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
         }
 #pragma unroll
-        for (int k = 0; k < UPT; ++k)
-          if (ck * 9 + tap == k * 9 * NCK / UPT) tv[k] = xform_unit(fill, it + 1, k);   // compile-time
+        for (int k = 0; k < UPT; ++k)                      // (the last iteration refills nothing)
+          if (decltype(LX)::value && ck * 9 + tap == k * 9 * NCK / UPT) tv[k] = xform_unit(fill, it + 1, k);
       }
     }
     if constexpr (RES == 2) {  // ResnetBlock.res_conv 1x1 on the raw block input (fragments prefetched)
@@ -334,7 +340,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         s2[fc][1] = __builtin_elementwise_fma(d1, d1, s2[fc][1]);
       }
     }
-    store_rows(tv, it + 1);
+    if constexpr (decltype(LX)::value) store_rows(tv, it + 1);
     lds_sync();                                          // LDS only: the prefetches stay in flight
   };
   issue_rows(rowsA, 1);
@@ -346,10 +352,14 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   static_assert(NYOUNG < 64, "vmcnt is a 6-bit counter");
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(NYOUNG) : "memory");
   SDDM_STAMP(a, 3);
-  for (int it = 0; it < iters; it += 2) {                // period-2 rotation of the register sets
-    body(it, rowsB, rowsA, r1A, r1B, r2A, r2B);
-    body(it + 1, rowsA, rowsB, r1B, r1A, r2B, r2A);
+  using yes = std::integral_constant<bool, true>;
+  using no = std::integral_constant<bool, false>;
+  for (int it = 0; it < iters - 2; it += 2) {            // period-2 rotation of the register sets
+    body(yes{}, yes{}, it, rowsB, rowsA, r1A, r1B, r2A, r2B);
+    body(yes{}, yes{}, it + 1, rowsA, rowsB, r1B, r1A, r2B, r2A);
   }
+  body(no{}, yes{}, iters - 2, rowsB, rowsA, r1A, r1B, r2A, r2B);
+  body(no{}, no{}, iters - 1, rowsA, rowsB, r1B, r1A, r2B, r2A);
 
   SDDM_STAMP(a, 4);
   // ---- GroupNorm statistics of the strip: lanes -> waves -> block ----
