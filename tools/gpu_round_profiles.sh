@@ -1,5 +1,5 @@
-# round evidence: headline bench (T=1000, CPU baseline), rocprofv3 kernel stats of the same workload
-# (T=100), PMC traffic, fp32 config #2 throughput, DiffWave and WaveGrad benches + kernel stats.
+# round evidence: PMC traffic, headline bench (T=1000, CPU baseline), rocprofv3 kernel stats of the
+# same workload (T=100), fp32 config #2 throughput, DiffWave and WaveGrad benches + kernel stats.
 # Usage: ROUND=r02 bash tools/gpu_round_profiles.sh ; results land in gpurun_out/profiles/
 set -o pipefail
 cd $GRAFT_REPO_ROOT
@@ -7,11 +7,13 @@ export TMPDIR=/tmp
 R=${ROUND:-r02}
 O=gpurun_out/profiles
 mkdir -p $O
+# PMC traffic first, written where bench.py reads it, so the headline line carries it
+TRAFFIC_OUT=profiles/${R}_hbm_traffic.json bash tools/gpu_traffic.sh || { echo TRAFFIC_FAIL; exit 1; }
+cp profiles/${R}_hbm_traffic.json $O/
 timeout -k 10 900 python3 bench.py > $O/${R}_bench.json.log 2>&1 || { echo BENCH_FAIL; tail -5 $O/${R}_bench.json.log; exit 1; }
 tail -1 $O/${R}_bench.json.log | cut -c1-200
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_bench -o run -- python3 bench.py --timesteps 100 --steps 1 --warmup 1 --no-cpu-baseline > $O/${R}_bench_T100_rocprof.json.log 2>&1 || { echo PROF_FAIL; exit 1; }
 cp gpurun_out/prof_bench/run_kernel_stats.csv $O/${R}_kernel_stats_T100_B16_bf16.csv
-TRAFFIC_OUT=$O/${R}_hbm_traffic.json bash tools/gpu_traffic.sh || { echo TRAFFIC_FAIL; exit 1; }
 timeout -k 10 900 python3 bench.py --dtype f32 --no-cpu-baseline > $O/${R}_unet_fp32_bench.json.log 2>&1 || { echo FP32_FAIL; exit 1; }
 tail -1 $O/${R}_unet_fp32_bench.json.log | cut -c1-200
 timeout -k 10 900 python3 bench.py --workload diffwave > $O/${R}_diffwave_bench.json.log 2>&1 || { echo DW_FAIL; tail -5 $O/${R}_diffwave_bench.json.log; exit 1; }
