@@ -257,7 +257,7 @@ def main_spec(args):
         tfs = args.steps * T * B * W["gflop"] / elapsed / 1e3      # whole-job MFMA rate per GPU
         gbs = args.steps * B * (T * W["melems"] + W["inv_melems"]) * 1e6 * es / elapsed / 1e9
         cpu = None
-        if not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline:             # CPU baseline: rank 0 at N=1 only
             v, dt, reps = cpu_baseline_spec(args.workload, model, spec_all, T)
             cpu_model, ncpu, naff = cpu_info()
             threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or ncpu
@@ -380,7 +380,7 @@ def main():
         roofline = unet_roofline(model, cond_all[:B].contiguous(), N, B, T, args.dtype, 1e3 * elapsed / args.steps)
 
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:   # CPU baseline: rank 0 at N=1 only
         log("CPU baseline")
         v, dt, threads = cpu_baseline(B, args.cpu_steps, N, T)
         cpu_model, ncpu, naff = cpu_info()
