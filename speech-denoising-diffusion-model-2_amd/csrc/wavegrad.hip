@@ -195,9 +195,11 @@ __global__ __launch_bounds__(256) void wg_conv_kernel(WGConvArgs a) {
 constexpr int WGL_MC = 128, WGL_HALO = 8;
 
 // TW = waves along time: block = 2 x TW waves = 128 channels x 64 TW positions (TW = 4 halves the
-// per-position weight traffic from L2 on the long levels)
+// per-position weight traffic from L2 on the long levels).  The 3-tap variants without FiLM are
+// held to 168 registers (three waves per SIMD, three blocks per CU: 135 vs 148 and 103 vs 114 us
+// per launch); the FiLM variant spills there (364 vs 252 us) and the 1-tap ones gain nothing
 template <typename T, int PRE, int KT, int TW>
-__global__ __launch_bounds__(128 * TW) void wg_conv_lds_kernel(WGConvArgs a) {
+__global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2) void wg_conv_lds_kernel(WGConvArgs a) {
 #pragma clang fp contract(off)
   constexpr int NT = 128 * TW, WGL_MT = 64 * TW;
   constexpr int ES = (int)sizeof(T), UE = 16 / ES;         // elements per 16-byte unit
