@@ -203,9 +203,13 @@ def main_spec(args):
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        # RCCL over xGMI; SDDM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+        # sharing one GPU (RCCL refuses two ranks on one device)
+        dist.init_process_group(os.environ.get("SDDM_DIST_BACKEND", "nccl"))
+    ndev = torch.cuda.device_count()
+    local_dev = local_rank % max(ndev, 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     cfg = read_json(os.path.join(PKG, "configs", W["config"]))
     if args.timesteps_set:
         cfg["diffusion"]["args"]["n_timestep"] = args.timesteps
@@ -247,7 +251,7 @@ def main_spec(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() != "gloo" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     if not torch.isfinite(result["out"]).all():
@@ -325,9 +329,13 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        # RCCL over xGMI; SDDM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
+        # sharing one GPU (RCCL refuses two ranks on one device)
+        dist.init_process_group(os.environ.get("SDDM_DIST_BACKEND", "nccl"))
+    ndev = torch.cuda.device_count()
+    local_dev = local_rank % max(ndev, 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
 
     cfg = read_json(os.path.join(PKG, "configs", "config_unet_bench.json"))
     cfg["diffusion"]["args"]["n_timestep"] = args.timesteps
@@ -367,7 +375,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() != "gloo" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
     if not torch.isfinite(result["out"]).all():
