@@ -126,3 +126,31 @@ def test_spectrogram_bin_count_is_checked(torch_cuda):
     m = M.SDDM_spectrogram(d, n, hop_samples=256, noise_condition="time_step").cuda()
     with pytest.raises(RuntimeError):
         m.infer(spec, seed=1)
+
+
+def test_sddm_spectrogram_training_forward(torch_cuda):
+    """SDDM_spectrogram inherits SDDM.forward (model.py:29-48): q-sample on HIP, then DiffWave on HIP
+    with the time_step noise condition (level = t + r, continuous: diffwave.py:41-45 has no lookup),
+    against oracle q_stochastic composed with oracle/diffwave.forward."""
+    import model.diffusion as D
+    import model.model as M
+    from oracle import diffwave as odw, sampler as osamp
+    from oracle.schedule import BUFFER_NAMES
+    z = golden("diffwave.npz")
+    k = "dw/fw/6x2"
+    spec = z[f"{k}/spec"]
+    B, N = spec.shape[0], 256 * spec.shape[-1]
+    d = D.GaussianDiffusion("linear", 50, 1e-4, 0.05, device="cuda")
+    m = M.SDDM_spectrogram(d, _net(), hop_samples=256, noise_condition="time_step").cuda()
+    rng = np.random.default_rng(8)
+    target = (0.3 * rng.standard_normal((B, 1, N))).astype(np.float32)
+    noise = rng.standard_normal((B, 1, N)).astype(np.float32)
+    t = np.array([3, 41], dtype=np.int64)[:B]
+    r = rng.random(B).astype(np.float32)
+    tg = lambda a: torch.from_numpy(a).cuda()
+    pred, nz = m(tg(target), tg(spec), noise=tg(noise), t=tg(t), random_step=tg(r))
+    tab = {n: getattr(d, n).cpu().numpy() for n in BUFFER_NAMES}
+    x_t, _, level = osamp.q_stochastic(tab, target, noise, t, r)
+    ref = odw.forward(diffwave_params(), spec, x_t, np.asarray(level, np.float32).reshape(-1))
+    assert pred.shape == (B, 1, N) and np.array_equal(nz.cpu().numpy(), noise)
+    assert rms(pred.cpu().numpy(), ref) <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))))
