@@ -80,7 +80,50 @@ def cpu_baseline(B_cpu, k_steps, N, T):
         eps = net(cond, x, np.full(B_cpu, tab["sqrt_alpha_bar"][t], np.float32))
         x = sampler.transition("condition_in", tab, x, t, eps, cond, philox.normal(7, t, x.shape))
     dt = (time.perf_counter() - t0) / k_steps
-    return B_cpu * N / 16000.0 / (dt * T), dt, threads
+    # a second timing at 8 threads (the survey's reference measurement used 8 Xeon threads): on a
+    # shared host the job's CPU quota, not the core count, limits the wider run
+    dt8 = None
+    if threads != 8:
+        torch.set_num_threads(8)
+        log("CPU step at 8 threads")
+        t1 = time.perf_counter()
+        net(cond, x, np.full(B_cpu, tab["sqrt_alpha_bar"][T - k_steps], np.float32))
+        dt8 = time.perf_counter() - t1
+        torch.set_num_threads(threads)
+    return B_cpu * N / 16000.0 / (dt * T), dt, threads, dt8
+
+
+def cpu_quota():
+    """The CPU share the host grants this job (cgroup v2 cpu.max: quota / period), None if unlimited."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def init_ranks():
+    """One process per GPU (torchrun env): bind this rank's device FIRST, then join the process
+    group with that device (RCCL over xGMI creates its communicator on it).  SDDM_DIST_BACKEND=gloo
+    rehearses the multi-rank path with several ranks sharing one GPU (RCCL refuses two ranks on one
+    device); ranks wrap onto the visible devices."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = torch.cuda.device_count()
+    local_dev = local_rank % max(ndev, 1)
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
+    if world > 1:
+        backend = os.environ.get("SDDM_DIST_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    return world, rank, dev
 
 
 def log(msg):
@@ -89,14 +132,22 @@ def log(msg):
 
 
 def kernel_src_hash():
-    """Hash of the HIP sources: a committed PMC traffic summary is used only for the kernels it measured."""
+    """Hash of everything that decides which kernel runs each layer and how: the HIP sources, the
+    runtime that plans the layers (sddm_runtime.cpp: choose_conv / choose_tile / choose_deep) and the
+    measured per-layer kernel table (configs/conv_tuning.json).  A committed PMC traffic summary is
+    used only for the kernels and layer plan it measured."""
     import glob
     import hashlib
     h = hashlib.sha256()
-    for f in sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h"))):
+    files = sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h")))
+    files += [os.path.join(PKG, "csrc", "sddm_runtime.cpp"), os.path.join(PKG, "configs", "conv_tuning.json")]
+    for f in files:
         with open(f, "rb") as fh:
             h.update(fh.read())
     return h.hexdigest()[:16]
+
+
+TRAFFIC_FILES = ("r03_hbm_traffic.json", "r02_hbm_traffic.json")   # newest first
 
 
 def unet_roofline(model, cond, N, B, T, dtype, ms_per_run):
@@ -129,19 +180,46 @@ def unet_roofline(model, cond, N, B, T, dtype, ms_per_run):
     step_bytes, step_flops = sum(o["bytes"] for o in ops), sum(o["flops"] for o in ops)
     step_ms = ms_per_run / T
     traffic, tsrc = None, None
-    tf = os.path.join(REPO, "profiles", "r02_hbm_traffic.json")
-    if os.path.exists(tf):
+    key = {"N": N, "B": B, "dtype": dtype, "src": kernel_src_hash()}
+    for name in TRAFFIC_FILES:
+        tf = os.path.join(REPO, "profiles", name)
+        if not os.path.exists(tf):
+            continue
         with open(tf) as fh:
             pmc = json.load(fh)
-        key = {"N": N, "B": B, "dtype": dtype, "src": kernel_src_hash()}
         if all(pmc.get(k) == v for k, v in key.items()) and dom in pmc.get("kernels", {}):
             traffic = round(pmc["kernels"][dom]["bytes_per_launch"])
-            tsrc = "profiles/r02_hbm_traffic.json (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel sources and workload)"
-    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+            tsrc = (f"profiles/{name} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE, same kernel sources, "
+                    f"layer plan and workload)")
+            break
+    # the top single template instantiation (the family above merges e.g. the strip kernel's
+    # residual-mode / GroupNorm variants, which rocprofv3 lists separately)
+    inst = {}
+    for o in ops:
+        a = inst.setdefault(o.get("inst") or o["kernel"], {"ms": 0.0, "n": 0, "bytes": 0.0, "layers": []})
+        a["ms"] += o["avg_ms"] * o["launches"]
+        a["n"] += o["launches"]
+        a["bytes"] += o["bytes"] * o["launches"]
+        a["layers"].append(o["name"])
+    top = max(inst, key=lambda k: inst[k]["ms"])
+    ti = inst[top]
+    ti_ms, ti_b = ti["ms"] / ti["n"], ti["bytes"] / ti["n"]
+    ti_gbs = ti_b / (ti_ms * 1e-3) / 1e9
+    top_inst = {"kernel": top, "layers": ti["layers"], "avg_launch_ms": round(ti_ms, 5),
+                "alg_bytes_per_launch": round(ti_b), "achieved": round(ti_gbs, 1),
+                "frac": round(ti_gbs / HBM_PEAK_GBS, 4), "share_of_launch_time": round(ti["ms"] / total_ms, 4)}
+    fam = {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+           "frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if dtype == "f32":
+        # the fp32 UNet (82.8 FLOP/B against an fp32 ridge of ~20) is MFMA-fp32 bound
+        fam = {"bound": "mfma", "achieved": round(tfs, 2), "peak": MFMA_PEAK_TFLOPS[dtype], "unit": "TFLOP/s",
+               "frac": round(tfs / MFMA_PEAK_TFLOPS[dtype], 4), "hbm_gbs": round(gbs, 1),
+               "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    return {**fam, "traffic": traffic, "traffic_source": tsrc,
             "kernel": dom, "layers": d["layers"], "avg_launch_ms": round(avg_ms, 5), "launches_timed": d["n"],
             "share_of_launch_time": round(d["ms"] / total_ms, 4), "alg_bytes_per_launch": round(bpl),
             "mfma_tflops": round(tfs, 2), "mfma_frac": round(tfs / MFMA_PEAK_TFLOPS[dtype], 4),
+            "top_instantiation": top_inst,
             "step": {"alg_bytes": round(step_bytes), "alg_flops": round(step_flops), "ms": round(step_ms, 5),
                      "achieved_gbs": round(step_bytes / (step_ms * 1e-3) / 1e9, 1),
                      "frac": round(step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
@@ -156,10 +234,10 @@ def unet_roofline(model, cond, N, B, T, dtype, ms_per_run):
 SPEC_WORKLOADS = {
     "diffwave": dict(config="config_diffwave_bench.json", frames=63, batch=64, bins=513, gflop=31.85,
                      melems=220.9, inv_melems=319.5, bound="hbm",
-                     label="DiffWave config_diffwave.json, linear 1e-4..0.02, T=200, time_step conditioning"),
+                     label="DiffWave config_diffwave.json, linear 1e-4..0.02, T={T}, time_step conditioning"),
     "wavegrad": dict(config="config_wavegrad_bench.json", frames=54, batch=64, bins=128, gflop=47.38,
                      melems=92.8, inv_melems=0.0, bound="mfma",
-                     label="WaveGrad, linear 1e-4..0.05, T=50 (SURVEY §8d fast schedule), sqrt_alpha_bar"),
+                     label="WaveGrad, linear 1e-4..0.05, T={T} (SURVEY §8d fast schedule: T=50), sqrt_alpha_bar"),
 }
 
 
@@ -199,17 +277,7 @@ def main_spec(args):
     import model.model as module_arch
 
     W = SPEC_WORKLOADS[args.workload]
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # RCCL over xGMI; SDDM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
-        # sharing one GPU (RCCL refuses two ranks on one device)
-        dist.init_process_group(os.environ.get("SDDM_DIST_BACKEND", "nccl"))
-    ndev = torch.cuda.device_count()
-    local_dev = local_rank % max(ndev, 1)
-    torch.cuda.set_device(local_dev)
-    dev = torch.device("cuda", local_dev)
+    world, rank, dev = init_ranks()
     cfg = read_json(os.path.join(PKG, "configs", W["config"]))
     if args.timesteps_set:
         cfg["diffusion"]["args"]["n_timestep"] = args.timesteps
@@ -275,7 +343,7 @@ def main_spec(args):
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
                 "data": "synthetic spectrograms U[0,1], random-init weights",
-                "config": {"workload": f"{W['label']}, {B}x{N}-sample clips per GPU",
+                "config": {"workload": f"{W['label'].format(T=T)}, {B}x{N}-sample clips per GPU",
                            "model": network.__class__.__name__, "global_batch": B * world, "seq_len": N,
                            "timesteps": T, "parallelism": f"dp{world}"},
                 "roofline": ({"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -325,17 +393,7 @@ def main():
     import model.model as module_arch
     from sddm_hip.synth import noisy_speech
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        # RCCL over xGMI; SDDM_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks
-        # sharing one GPU (RCCL refuses two ranks on one device)
-        dist.init_process_group(os.environ.get("SDDM_DIST_BACKEND", "nccl"))
-    ndev = torch.cuda.device_count()
-    local_dev = local_rank % max(ndev, 1)
-    torch.cuda.set_device(local_dev)
-    dev = torch.device("cuda", local_dev)
+    world, rank, dev = init_ranks()
 
     cfg = read_json(os.path.join(PKG, "configs", "config_unet_bench.json"))
     cfg["diffusion"]["args"]["n_timestep"] = args.timesteps
@@ -390,17 +448,22 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # CPU baseline: rank 0 at N=1 only
         log("CPU baseline")
-        v, dt, threads = cpu_baseline(B, args.cpu_steps, N, T)
+        v, dt, threads, dt8 = cpu_baseline(B, args.cpu_steps, N, T)
         cpu_model, ncpu, naff = cpu_info()
         cpu = {"value": round(v, 6), "unit": "audio_s/s", "cores": threads, "kind": "port",
-               "cpu_model": cpu_model, "cpu_count": ncpu, "cpu_affinity": naff,
+               "cpu_model": cpu_model, "cpu_count": ncpu, "cpu_affinity": naff, "cpu_quota_cores": cpu_quota(),
                "sample": f"PyTorch-CPU restatement of UNetModified2 (oracle/unet_torch.py, pinned to the "
                          f"reference goldens), {args.cpu_steps} reverse steps at B={B}x{N} ({dt:.2f} s/step, "
-                         f"torch.set_num_threads({threads})), extrapolated x{T}/{args.cpu_steps}"}
+                         f"torch.set_num_threads({threads})), extrapolated x{T}/{args.cpu_steps}",
+               "note": "the GPU box shares its host: os.cpu_count() shows the whole machine, the job runs under "
+                       "a CPU quota (cpu_quota_cores) beside other jobs, so this understates an idle host (the "
+                       "survey timed the reference itself at 0.654 s/step on 8 idle Xeon threads)"}
+        if dt8 is not None:
+            cpu["threads_8"] = {"s_per_step": round(dt8, 3), "value": round(B * N / 16000.0 / (dt8 * T), 6)}
 
     if rank == 0:
         audio_s = args.steps * B * world * N / 16000.0
-        line = {"metric": "denoised audio sec/sec, 1000-step UNetModified2 @16kHz",
+        line = {"metric": f"denoised audio sec/sec, {T}-step UNetModified2 @16kHz",
                 "value": round(audio_s / elapsed, 4), "unit": "audio_s/s", "n_gpus": world,
                 "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,

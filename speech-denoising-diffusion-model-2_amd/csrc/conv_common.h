@@ -355,6 +355,14 @@ namespace sddm {
 // the stores just issued, on the critical path of the block, for nothing.
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Workgroup barrier for an LDS-DMA hand-off (global_load_lds): every wave's DMA loads into LDS are
+// counted by vmcnt, not lgkmcnt, so a wave must drain vmcnt before the barrier for the other
+// waves to read what it loaded.  Explicit (not __syncthreads()) so that the barrier cannot be
+// turned into lds_sync() by mistake and does not depend on how the fence happens to lower.
+__device__ __forceinline__ void dma_sync() {
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 __device__ __forceinline__ float silu_fast(float x) { return x * __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 
 // SiLU of two values with packed fp32 arithmetic around the two transcendentals per value:

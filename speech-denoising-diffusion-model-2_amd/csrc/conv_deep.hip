@@ -463,6 +463,13 @@ hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B
   return deep_dispatch<f16_t>(mt, nw, nb, s2, a, B, s, nullptr);
 }
 
+int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps) {
+  const int spw = (ksteps + nw - 1) / nw;
+  if (dtype == DT_F32) return 4;
+  if (nw == 4 || mt >= 128) return 8;
+  return deep_ring<bf16_t, 64, 8>(spw);
+}
+
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a) {
   size_t lo = (size_t)1 << 40;
   const int nw = a.deep_nw, nb = a.deep_nb ? a.deep_nb : 32;

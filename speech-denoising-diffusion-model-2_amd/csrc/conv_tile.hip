@@ -299,7 +299,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   SDDM_STAMP(a, 1);
   __syncthreads();                                         // gsc visible
   transform(0, 0);
-  __syncthreads();                                         // operand image 0, weights 0
+  dma_sync();                                              // operand image 0, weights 0 (LDS-DMA)
   SDDM_STAMP(a, 2);
   for (int k = 0; k < nk; ++k) {
     const int cur = k & 1, nxt = cur ^ 1;
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     }
     mma(k, cur);
     if (k + 1 < nk) transform(k + 1, nxt);                 // IB[nxt] was read by chunk k - 1
-    __syncthreads();
+    dma_sync();                                            // WB[nxt] landed by LDS-DMA from every wave
   }
   SDDM_STAMP(a, 4);
 

@@ -97,6 +97,7 @@ size_t conv_tile_lds_bytes(int cfg, bool s2, const ConvArgs& a);
 // mt: output pixels per block (32 / 64 / 128); s2: stride-2 Downsample
 hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B, hipStream_t s);
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a);
+int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps);   // the D template argument (profiles)
 
 // ---- row-streaming 3x3 convolution for segment widths 64 / 128 (conv_strip.hip) ----
 hipError_t launch_conv_strip(int dtype, int nblk, int mpi, int SR, const ConvArgs& a, int B, hipStream_t s);

@@ -208,7 +208,8 @@ struct Op {
   std::function<hipError_t(hipStream_t)> run;
   std::string name = "";
   std::function<hipError_t(hipStream_t, int)> run_dbg = nullptr;   // ablation relaunch (timing experiments)
-  std::string kname = "";   // kernel (template instantiation) the op launches, for per-kernel profiles
+  std::string kname = "";   // kernel family the op launches (template arguments that pick the tiling)
+  std::string kinst = "";   // the exact template instantiation (as rocprofv3 lists it), for per-kernel profiles
 };
 struct ProfAcc { double ms = 0; int64_t n = 0; double bytes = 0, flops = 0; };
 
@@ -802,6 +803,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           return launch_conv_in(dt, x, B, s);
                         }, "downs.0"});
       L.ops.back().kname = std::string("conv_in_kernel<") + dt_name(dt) + ">";
+      L.ops.back().kinst = L.ops.back().kname;
     } else if (st.type == ST_CONV) {
       ConvArgs a{};
       const Tensor sa = TT(st.srcA), sb = TT(st.srcB), o = TT(st.out);
@@ -884,6 +886,19 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         } else
           snprintf(kn, sizeof(kn), "conv_deep_kernel<%s,%d,%d,%d,%d>", dt_name(dt), s2 ? 1 : 0, ch.mt, ch.nw, ch.nb);
         L.ops.back().kname = kn;
+        // instantiation: the strip kernel's residual mode / GroupNorm and the deep kernel's weight
+        // ring depth are template arguments the family name leaves out
+        char ki[192];
+        if (ch.strip)
+          snprintf(ki, sizeof(ki), "conv_strip_kernel<%s,%d,%d,%d,%d,%d,%d>", dt_name(dt), ch.nblk / 16, a.Wo, Cin,
+                   ch.mpi, a.res_mode, a.gamma ? 1 : 0);
+        else if (ch.tile >= 0)
+          snprintf(ki, sizeof(ki), "%s", kn);
+        else
+          snprintf(ki, sizeof(ki), "conv_deep_kernel<%s,%d,%d,%d,%d,%d>", dt_name(dt), s2 ? 1 : 0, ch.mt, ch.nw,
+                   conv_deep_ring_depth(dt, ch.mt, ch.nw, (Cin / 32) * 9 + (a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0)),
+                   ch.nb);
+        L.ops.back().kinst = ki;
       }
       {  // flags: 1 no stats, 2 no GroupNorm transform, 4 no residual / embedding, 8 skip the K loop
         auto base = L.ops.back().run;
@@ -937,6 +952,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           return launch_final(dt, x, B, s);
                         }, "final_conv"});
       L.ops.back().kname = std::string("final_kernel<") + dt_name(dt) + (f.FT >= 16 ? ",1024>" : ",512>");
+      L.ops.back().kinst = L.ops.back().kname;
     }
   }
   return SDDM_OK;
@@ -1645,9 +1661,9 @@ int sddm_profile_ops(sddm_ctx* c, char* buf, int64_t buflen) {
   for (size_t i = 0; i < ops.size(); ++i) {
     const ProfAcc a = i < c->op_acc.size() ? c->op_acc[i] : ProfAcc{};
     snprintf(tmp, sizeof(tmp),
-             "%s{\"name\": \"%s\", \"kernel\": \"%s\", \"cls\": %d, \"launches\": %lld, \"avg_ms\": %.6f, "
-             "\"bytes\": %.0f, \"flops\": %.0f}",
-             i ? ", " : "", ops[i].name.c_str(), ops[i].kname.c_str(), ops[i].cls, (long long)a.n,
+             "%s{\"name\": \"%s\", \"kernel\": \"%s\", \"inst\": \"%s\", \"cls\": %d, \"launches\": %lld, "
+             "\"avg_ms\": %.6f, \"bytes\": %.0f, \"flops\": %.0f}",
+             i ? ", " : "", ops[i].name.c_str(), ops[i].kname.c_str(), ops[i].kinst.c_str(), ops[i].cls, (long long)a.n,
              a.n ? a.ms / a.n : 0.0, ops[i].bytes, ops[i].flops);
     js += tmp;
   }

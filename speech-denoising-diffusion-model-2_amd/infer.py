@@ -103,9 +103,11 @@ def main(config, seed=None):
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:                                   # torchrun: one process per GPU, RCCL over xGMI
         import torch.distributed as dist
-        if not dist.is_initialized():
-            dist.init_process_group("nccl")
+        # bind the rank's device before the process group, and hand it to RCCL (its communicator
+        # lives on that device)
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        if not dist.is_initialized():
+            dist.init_process_group("nccl", device_id=torch.device("cuda", torch.cuda.current_device()))
     device = torch.device("cuda", torch.cuda.current_device())
     _, _, model = module_arch.build_from_config(config, module_diffusion, module_network, module_arch, device)
     model = model.to(device).eval()

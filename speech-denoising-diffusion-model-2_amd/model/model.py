@@ -77,12 +77,21 @@ class SDDM(nn.Module):
             self._ctx, self._ctx_key = ctx, key
         return self._ctx
 
-    @torch.no_grad()
     def forward(self, target, condition, noise=None, t=None, random_step=None):
         """Training-step forward (model.py:29-48): q-sample x_t from the target, estimate its noise.
         Returns (predicted, noise) like the reference.  Both pieces run on HIP (sddm_q_sample, then
         the network forward); the draws (randn_like / randint / rand on the target's device) are the
-        reference's unless given.  Inference-only: the HIP path has no backward, so no autograd."""
+        reference's unless given.  Evaluation only: the HIP path has no backward, so a call that
+        would build an autograd graph (grad mode on, parameters requiring grad: the reference's
+        Trainer._train_epoch, trainer.py:64-73) raises instead of returning tensors without history."""
+        if torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters()):
+            raise NotImplementedError(
+                "SDDM.forward on HIP has no backward (no training step): call it under torch.no_grad() "
+                "or with the parameters' requires_grad off")
+        with torch.no_grad():
+            return self._forward_eval(target, condition, noise, t, random_step)
+
+    def _forward_eval(self, target, condition, noise, t, random_step):
         if not target.is_cuda:
             raise RuntimeError("SDDM.forward runs on the HIP device; move the tensors to cuda")
         if noise is None:
@@ -209,8 +218,9 @@ def spectrogram_kwargs(config, diffusion):
     """(network kwargs, arch kwargs) for init_obj of a spectrogram-conditioned model."""
     cfg = config.config if hasattr(config, "config") else config
     spec = cfg.get("spectrogram", {})
-    if cfg.get("datatype", ".spec.npy") == ".mel.npy":
-        bins = cfg["mel_spectrogram"]["n_mels"]
+    if cfg.get("datatype", ".spec.npy") == ".mel.npy" or _dataset_datatype(cfg) == ".mel.npy":
+        spec = cfg.get("mel_spectrogram", spec)
+        bins = spec["n_mels"]
     else:
         bins = spec.get("freq_bins", spec.get("stft_bins", spec.get("window_length", 1024) // 2 + 1))
     net_kw = {"num_samples": cfg.get("num_samples", -1), "freq_bins": bins, "num_timesteps": diffusion.num_timesteps}
@@ -218,6 +228,19 @@ def spectrogram_kwargs(config, diffusion):
     if "hop_samples" not in cfg["arch"].get("args", {}):
         arch_kw["hop_samples"] = spec.get("hop_samples", 300 if cfg["network"]["type"] == "WaveGrad" else 256)
     return net_kw, arch_kw
+
+
+def _dataset_datatype(cfg):
+    """The spectrogram file type the config's datasets read (config_diffwave.json:44,51 put
+    'datatype' under the dataset args, train_specmodel.py:21 reads a top-level one): the top-level
+    key, else infer_dataset's, else tr_dataset's."""
+    if "datatype" in cfg:
+        return cfg["datatype"]
+    for k in ("infer_dataset", "tr_dataset", "val_dataset"):
+        dt = cfg.get(k, {}).get("args", {}).get("datatype")
+        if dt:
+            return dt
+    return None
 
 
 def build_from_config(config, module_diffusion, module_network, module_arch, device):

@@ -101,8 +101,24 @@ def test_training_forward_needs_the_hip_device():
     silent CPU fallback."""
     m = _build()
     x = torch.zeros(1, 1, 2112)
-    with pytest.raises(RuntimeError):
+    with torch.no_grad(), pytest.raises(RuntimeError) as e:
         m(x, x)
+    assert not isinstance(e.value, NotImplementedError)
+
+
+def test_training_forward_refuses_autograd():
+    """The HIP training-step forward has no backward: in grad mode with trainable parameters (the
+    reference's Trainer._train_epoch, trainer.py:64-73) it raises NotImplementedError up front
+    instead of returning tensors that fail later at loss.backward()."""
+    m = _build()
+    x = torch.zeros(1, 1, 2112)
+    with pytest.raises(NotImplementedError):
+        m(x, x)
+    for p in m.parameters():
+        p.requires_grad_(False)
+    with pytest.raises(RuntimeError) as e:          # past the autograd check: host tensors refused
+        m(x, x)
+    assert not isinstance(e.value, NotImplementedError)
 
 
 def test_facade_geometry_assert_like_reference():

@@ -148,7 +148,8 @@ def test_sddm_spectrogram_training_forward(torch_cuda):
     t = np.array([3, 41], dtype=np.int64)[:B]
     r = rng.random(B).astype(np.float32)
     tg = lambda a: torch.from_numpy(a).cuda()
-    pred, nz = m(tg(target), tg(spec), noise=tg(noise), t=tg(t), random_step=tg(r))
+    with torch.no_grad():
+        pred, nz = m(tg(target), tg(spec), noise=tg(noise), t=tg(t), random_step=tg(r))
     tab = {n: getattr(d, n).cpu().numpy() for n in BUFFER_NAMES}
     x_t, _, level = osamp.q_stochastic(tab, target, noise, t, r)
     ref = odw.forward(diffwave_params(), spec, x_t, np.asarray(level, np.float32).reshape(-1))

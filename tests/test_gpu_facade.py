@@ -128,17 +128,21 @@ def test_sddm_forward_training_step(torch_cuda, q_transition, noise_condition):
     r = rng.random(B).astype(np.float32)
     tab = {k: getattr(d, k).cpu().numpy() for k in BUFFER_NAMES}
     tg = lambda a: torch.from_numpy(a).to(dev)
+    with pytest.raises(NotImplementedError):         # no HIP backward: grad mode refused
+        m(tg(target), tg(cond), noise=tg(noise), t=tg(t), random_step=tg(r))
     if q_transition == "original":
-        pred, nz = m(tg(target), tg(cond), noise=tg(noise), t=tg(t), random_step=tg(r))
+        with torch.no_grad():
+            pred, nz = m(tg(target), tg(cond), noise=tg(noise), t=tg(t), random_step=tg(r))
         x_t, s, level = osamp.q_stochastic(tab, target, noise, t, r)
         nl = s if noise_condition == "sqrt_alpha_bar" else level
         ref_noise = noise
     else:
-        pred, nz = m(tg(target), tg(cond), noise=tg(noise), t=tg(t.reshape(B, 1, 1)))
+        with torch.no_grad():
+            pred, nz = m(tg(target), tg(cond), noise=tg(noise), t=tg(t.reshape(B, 1, 1)))
         x_t, ref_noise, nl = osamp.q_stochastic_conditional(tab, target, cond, noise, t)
     ref = ounet.forward(P, unet_arch(N), cond, x_t, np.asarray(nl, np.float32).reshape(-1))
     assert pred.shape == (B, 1, N) and nz.shape == (B, 1, N)
     assert np.abs(nz.cpu().numpy() - ref_noise).max() <= 1e-5
     assert rms(pred.cpu().numpy(), ref) <= 1e-4 * max(1.0, float(np.sqrt(np.mean(ref.astype(np.float64) ** 2))))
-    with pytest.raises(RuntimeError):
+    with torch.no_grad(), pytest.raises(RuntimeError):
         m(tg(target).cpu(), tg(cond).cpu())

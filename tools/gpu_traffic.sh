@@ -9,5 +9,5 @@ for c in FETCH_SIZE WRITE_SIZE; do
   rm -rf gpurun_out/traffic_$c
   timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/traffic_$c -o run -- python3 tools/profile_ops.py --timesteps 2 --json gpurun_out/traffic_ops_$c.json > gpurun_out/traffic_$c.log 2>&1 || { echo TRAFFIC_FAIL $c; tail -5 gpurun_out/traffic_$c.log; exit 1; }
 done
-python3 tools/traffic.py ${TRAFFIC_OUT:-profiles/r02_hbm_traffic.json} | cut -c1-600
+python3 tools/traffic.py ${TRAFFIC_OUT:-profiles/r03_hbm_traffic.json} | cut -c1-600
 echo TRAFFIC_OK

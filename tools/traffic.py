@@ -14,7 +14,7 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r02_hbm_traffic.json")
+out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r03_hbm_traffic.json")
 UNET = re.compile(r"conv_in_kernel|conv_strip_kernel|conv_tile_kernel|conv_deep_kernel|final_kernel")
 
 
