@@ -92,6 +92,9 @@ def main():
     if args.only == "wavegrad":
         gen_wavegrad(torch, philox, make_params, GaussianDiffusion, args.out)
         return
+    if args.only == "long":
+        gen_long(torch, philox, make_params, GaussianDiffusion, noisy_speech, args.out)
+        return
 
     # 1. schedule tables (diffusion.py:50-161)
     for s in SCHEDULES:
@@ -354,6 +357,91 @@ def gen_wavegrad(torch, philox, make_params, GaussianDiffusion, out_dir):
     keys["wavegrad"] = [[k, list(v.shape)] for k, v in net.state_dict().items()]
     with open(os.path.join(out_dir, "state_dict_keys.json"), "w") as f:
         json.dump(keys, f, indent=0)
+
+
+def gen_long(torch, philox, make_params, GaussianDiffusion, noisy_speech, out_dir):
+    """11. the long sampling loops the benches run, from the reference (long_loops.npz):
+    UNet condition_in at T=1000 (config_unet.json's linear 1e-6..1e-3 at the headline's T; N=2112,
+    B=2), DiffWave at T=200 (config_diffwave.json schedule and time_step condition; 63 frames, B=1)
+    and WaveGrad at T=50 (SURVEY §8d fast schedule linear 1e-4..0.05; 54 frames, B=2: the reference
+    WaveGrad cannot run B=1).  x_t is kept every `rec` steps to localise a divergence."""
+    from model.UNetModified2 import UNetModified2
+    from model.model import SDDM, SDDM_spectrogram
+    from model.diffwave import DiffWave
+    from model.wavegrad import WaveGrad
+    lg = {}
+
+    def recorder(d, every, T):
+        steps, orig = [], d.p_transition
+
+        def rec(x, t, *a, **kw):
+            y = orig(x, t, *a, **kw)
+            if t % every == 1 or every == 1:     # x_{t-1} after step t = k*every + 1: x_{k*every}
+                steps.append(y.numpy().copy())
+            return y
+        d.p_transition = rec
+        return steps
+
+    # UNet, T = 1000
+    sched, N, B = ("linear", 1000, 1e-6, 1e-3), 2112, 2
+    d = GaussianDiffusion(*sched, device="cpu")
+    net = UNetModified2(num_samples=N, **UNET_ARGS)
+    P = make_params({k: tuple(v.shape) for k, v in net.state_dict().items()}, 0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    m = SDDM(d, net, p_transition="condition_in").eval()
+    cond = noisy_speech(B, N, seed=1234)
+    steps = recorder(d, 100, sched[1])
+    inj = NoiseInjector(torch, philox, 7)
+    inj.draws = [0] + list(range(sched[1], 1, -1))
+    with inj, torch.no_grad():
+        y = m.infer(torch.from_numpy(cond))
+    key = f"long/unet/condition_in/{sched_key(sched)}/{N}x{B}"
+    lg[key + "/cond"], lg[key + "/out"], lg[key + "/every100"] = cond, y.numpy().copy(), np.stack(steps)
+    print("unet T=1000 done", flush=True)
+
+    # DiffWave, T = 200 (config_diffwave.json), 63 frames
+    sched, F, B = ("linear", 200, 1e-4, 0.02), 63, 1
+    net = DiffWave(num_samples=-1, num_timesteps=sched[1], freq_bins=513, residual_channels=64,
+                   residual_layers=30, dilation_cycle_length=10)
+    P = make_params({k: tuple(v.shape) for k, v in net.state_dict().items()}, 0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    net.eval()
+    spec = np.random.default_rng(21).uniform(0, 1, (B, 513, F)).astype(np.float32)
+    d = GaussianDiffusion(*sched, device="cpu")
+    m = SDDM_spectrogram(d, net, hop_samples=256, noise_condition="time_step").eval()
+    steps = recorder(d, 20, sched[1])
+    inj = NoiseInjector(torch, philox, 7)
+    inj.draws = [0] + list(range(sched[1], 1, -1))
+    with inj, torch.no_grad():
+        y = m.infer(torch.from_numpy(spec))
+    key = f"long/diffwave/time_step/{sched_key(sched)}/{F}x{B}"
+    lg[key + "/spec"], lg[key + "/out"], lg[key + "/every20"] = spec, y.numpy().copy(), np.stack(steps)
+    print("diffwave T=200 done", flush=True)
+
+    # WaveGrad, T = 50, 54 frames (adapter of SURVEY Q4, as gen_wavegrad)
+    sched, F, B = ("linear", 50, 1e-4, 0.05), 54, 2
+    net = WaveGrad()
+    P = make_params({k: tuple(v.shape) for k, v in net.state_dict().items()}, 0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    net.eval()
+    spec = np.random.default_rng(22).uniform(0, 1, (B, 128, F)).astype(np.float32)
+    N = 300 * F
+    d = GaussianDiffusion(*sched, device="cpu")
+    inj = NoiseInjector(torch, philox, 7)
+    inj.draws = [0] + list(range(sched[1], 1, -1))
+    steps = []
+    with inj, torch.no_grad():
+        x = torch.randn(B, 1, N)                                   # model.py:216
+        for t in reversed(range(1, sched[1] + 1)):
+            noise_level = d.get_noise_level(t) * torch.ones(B)     # model.py:227-229 (adapter: [B])
+            eps = net(torch.from_numpy(spec), x[:, 0, :], noise_level).reshape(B, 1, N)
+            x = d.p_transition(x, t, eps)
+            if t % 10 == 1:
+                steps.append(x.numpy().copy())
+    key = f"long/wavegrad/sqrt_alpha_bar/{sched_key(sched)}/{F}x{B}"
+    lg[key + "/spec"], lg[key + "/out"], lg[key + "/every10"] = spec, x.numpy().copy(), np.stack(steps)
+    np.savez_compressed(os.path.join(out_dir, "long_loops.npz"), **lg)
+    print("wrote", os.path.join(out_dir, "long_loops.npz"))
 
 
 if __name__ == "__main__":

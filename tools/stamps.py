@@ -45,6 +45,10 @@ def main():
     for op in a.ops:
         os.environ["SDDM_STAMPS"] = op
         ctx = sddm_hip.Context(unet_config(a.N), 0, dt)
+        tf = os.path.join(REPO, "speech-denoising-diffusion-model-2_amd", "configs", "conv_tuning.json")
+        if os.path.exists(tf) and not os.environ.get("SDDM_NO_TUNING"):    # the measured per-layer kernels
+            with open(tf) as f:
+                ctx.set_conv_tuning(f.read())
         for k, v in params.items():
             ctx.load_param("noise_estimate_model." + k, v)
         for _ in range(3):
