@@ -1,0 +1,63 @@
+"""Per-op timestamps inside the fused deep-level chain (conv_chain.hip), normal build.
+
+    SDDM_CHAIN_STAMPS=1 python tools/chain_stamps.py [--batch 16] [--dtype bf16]
+
+Per image: s_memrealtime (100 MHz) at each op's start and at the end of its K loop, and at the
+kernel's end; printed as the median over images of the K-loop time and the epilogue time per op.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "speech-denoising-diffusion-model-2_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=16)
+    ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--N", type=int, default=16448)
+    a = ap.parse_args()
+    os.environ["SDDM_CHAIN_STAMPS"] = "1"
+    import numpy as np
+    import torch
+    import sddm_hip
+    from _helpers import unet_config, unet_params
+    from sddm_hip.synth import noisy_speech
+    dt = {"bf16": "bfloat16", "f16": "float16"}[a.dtype]
+    dev = torch.device("cuda", 0)
+    L = sddm_hip.lib()
+    L.sddm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.POINTER(ctypes.c_int64)]
+    L.sddm_debug_stamps.restype = ctypes.c_int
+    ctx = sddm_hip.Context(unet_config(a.N), 0, dt)
+    for k, v in unet_params(a.N).items():
+        ctx.load_param("noise_estimate_model." + k, v)
+    cond = torch.from_numpy(noisy_speech(a.batch, a.N, seed=3)).to(dev)
+    x = torch.from_numpy(noisy_speech(a.batch, a.N, seed=4)).to(dev)
+    nl = torch.full((a.batch,), 0.5, device=dev)
+    eps = torch.empty_like(cond)
+    for _ in range(3):
+        ctx.network_forward(cond, x, nl, eps)
+    torch.cuda.synchronize()
+    names = [o["name"] for o in ctx.profile_ops()]
+    print("ops:", [n for n in names if n.startswith("chain")])
+    buf = np.zeros((65536, 8), dtype=np.uint64)
+    n = ctypes.c_int64()
+    sddm_hip.check(L.sddm_debug_stamps(ctx._h, buf.ctypes.data, 65536, ctypes.byref(n)))
+    st = buf[:n.value].reshape(a.batch, 32).astype(np.float64) * 0.01   # us
+    nops = int(os.environ.get("CHAIN_NOPS", "14"))
+    total = np.median(st[:, 31] - st[:, 0])
+    print(f"chain total (median over images) {total:.1f} us")
+    for i in range(nops):
+        k = np.median(st[:, 2 * i + 1] - st[:, 2 * i]) if st[0, 2 * i + 1] > 0 else 0.0
+        nxt = st[:, 2 * i + 2] if i + 1 < nops else st[:, 31]
+        e = np.median(nxt - (st[:, 2 * i + 1] if st[0, 2 * i + 1] > 0 else st[:, 2 * i]))
+        print(f"  op {i:2d}: K loop {k:7.2f} us  epilogue/rest {e:6.2f} us")
+
+
+if __name__ == "__main__":
+    main()
