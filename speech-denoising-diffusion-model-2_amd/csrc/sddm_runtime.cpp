@@ -298,8 +298,9 @@ struct sddm_ctx {
   std::map<std::string, KernTune> kern_tune;
   int tune_B = -1, tune_dtype = -1, tune_N = -1;
   // fused deep-level chain (conv_chain.hip): 1 = wherever the geometry allows, 0 = per-layer
-  // kernels only (tuning JSON key "chain"; SDDM_CHAIN=0 overrides)
-  int chain = 1;
+  // kernels only (tuning JSON key "chain"; SDDM_CHAIN overrides).  Off by default until it beats
+  // the per-layer kernels on the bench geometry.
+  int chain = 0;
   int hop_samples = 256;
 
   const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
@@ -1974,7 +1975,7 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
       if (t.kind == 2 && (t.a < 0 || t.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), t.a);
       c->kern_tune[kv.first] = t;
     }
-  c->chain = (int)j.number("chain", 1) != 0 ? 1 : 0;
+  c->chain = (int)j.number("chain", 0) != 0 ? 1 : 0;
   c->tune_B = (int)j.number("lane_batch", -1);
   c->tune_dtype = dt;
   c->tune_N = (int)j.number("num_samples", -1);
