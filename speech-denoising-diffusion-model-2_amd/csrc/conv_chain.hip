@@ -109,9 +109,42 @@ __device__ __forceinline__ void chain_reload(COp& op, CTen* tens, char* smem, in
 
 // weight fragment of K step s, 16-channel block nf (a function, not a lambda: a closure holding the
 // two base pointers would stay in scratch memory)
+// Per-op parameters staged in LDS one op ahead: [gamma Cin][beta Cin][bias + noise embedding Cout]
+// fp32 in one of two buffers (3 x cmax floats each) right after the GN scale / shift.  The loads
+// for op `nx` are issued at the start of the op before it and stored at its end, so no op waits
+// for a global round trip for its GroupNorm affine or epilogue constants.
+constexpr int kPrmPerThread = 4;   // 3 x cmax <= 4 x 256 (cmax <= 341)
+__device__ __forceinline__ void chain_prm_load(const ChainArgs& a, COp* ops, int nx, int trow, float (&v)[kPrmPerThread]) {
+#pragma unroll
+  for (int k = 0; k < kPrmPerThread; ++k) v[k] = 0.f;
+  if (nx >= a.nops) return;
+  COp& o = ops[nx];
+  CTen* tens = (CTen*)a.tens;
+  const int Cin = tens[o.a].C + (o.b >= 0 ? tens[o.b].C : 0), Cout = o.Cout;
+  const float* trw = a.temb + (size_t)trow * a.temb_ld + o.toff;
+#pragma unroll
+  for (int k = 0; k < kPrmPerThread; ++k) {
+    const int e = (int)threadIdx.x + k * kChainThreads;
+    if (o.gn && e < Cin) v[k] = gloadf(o.gamma + e);
+    else if (o.gn && e < 2 * Cin) v[k] = gloadf(o.beta + (e - Cin));
+    else if (e >= 2 * Cin && e < 2 * Cin + Cout) {
+      const int c = e - 2 * Cin;
+      v[k] = gloadf(o.bias + c) + (o.temb ? gloadf(trw + c) : 0.f);
+    }
+  }
+}
+__device__ __forceinline__ void chain_prm_store(const ChainArgs& a, char* smem, int par, const float (&v)[kPrmPerThread]) {
+  float* dst = (float*)(smem + a.gsc) + 2 * a.cmax + par * 3 * a.cmax;
+#pragma unroll
+  for (int k = 0; k < kPrmPerThread; ++k) {
+    const int e = (int)threadIdx.x + k * kChainThreads;
+    if (e < 3 * a.cmax) dst[e] = v[k];
+  }
+}
+
 template <typename T, int MFW, int NFW, int FX>
 __device__ __forceinline__ void chain_op(const ChainArgs& a, COp& op, CTen* tens, char* smem, int b, int trow,
-                                         unsigned long long* stamp) {
+                                         unsigned long long* stamp, int par, int nx) {
   constexpr int NT = kChainThreads, NG = kChainWaves, MAXU = 8, D = 9;
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
   const int ng = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -148,14 +181,10 @@ __device__ __forceinline__ void chain_op(const ChainArgs& a, COp& op, CTen* tens
   const int dbg = a.dbg;
 
   // bias + noise embedding of this lane's epilogue channels: issued first, used at the end
-  float badd[NFW][4];
-#pragma unroll
-  for (int j = 0; j < NFW; ++j) {
-    const int co = (ng + NG * j) * 16 + 4 * g;
-    const float* trw = a.temb + (size_t)trow * a.temb_ld + op.toff;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) badd[j][r] = gloadf(op.bias + co + r) + (op.temb ? gloadf(trw + co + r) : 0.f);
-  }
+  // this op's parameters (staged in LDS by the previous op); the next op's are loaded now
+  const float* prm = (const float*)(smem + a.gsc) + 2 * cmax + par * 3 * cmax;
+  float pnext[kPrmPerThread];
+  chain_prm_load(a, (COp*)a.ops, nx, trow, pnext);
 
   // ---- weight fragments: [Cout/16][K steps][64 lanes][8]; K step s = 9 * chunk + tap for the
   // 3x3 chunks, then one step per 1x1 res_conv chunk.  A ring of the next 9 steps per wave (slot =
@@ -185,8 +214,8 @@ __device__ __forceinline__ void chain_op(const ChainArgs& a, COp& op, CTen* tens
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int c = min(tid + h * NT, Cin - 1);
-      gm[h] = gloadf(op.gamma + c);
-      bt[h] = gloadf(op.beta + c);
+      gm[h] = prm[c];
+      bt[h] = prm[Cin + c];
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -315,6 +344,7 @@ __device__ __forceinline__ void chain_op(const ChainArgs& a, COp& op, CTen* tens
       if (kb > 0) lds_sync();       // every wave is done with the previous group
       if (!(dbg & 2)) stage(k0, k1);
       lds_sync();
+      if (stamp && kb == 0 && threadIdx.x == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
       load_b3(kb - k0, 0, Bb[0]);
     }
 #pragma unroll
@@ -348,14 +378,16 @@ __device__ __forceinline__ void chain_op(const ChainArgs& a, COp& op, CTen* tens
     for (int i = 0; i < MFW; ++i) Bb[0][i] = Bb[1][i];
   }
 
-  if (stamp && threadIdx.x == 0) stamp[1] = __builtin_amdgcn_s_memrealtime();
+  if (stamp && threadIdx.x == 0) stamp[2] = __builtin_amdgcn_s_memrealtime();
   // ---- 3. epilogue (acc becomes the fp32 output values) ----
 #pragma unroll
-  for (int i = 0; i < MFW; ++i)
+  for (int j = 0; j < NFW; ++j) {
+    const f32x4 bv = *(const f32x4*)(prm + 2 * Cin + (ng + NG * j) * 16 + 4 * g);   // bias + embedding
 #pragma unroll
-    for (int j = 0; j < NFW; ++j)
+    for (int i = 0; i < MFW; ++i)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[i][j][r] += badd[j][r];
+      for (int r = 0; r < 4; ++r) acc[i][j][r] += bv[r];
+  }
   if (res_mode == 1) {              // identity residual (ResnetBlock with dim == dim_out)
 #pragma unroll
     for (int i = 0; i < MFW; ++i) {
@@ -420,8 +452,10 @@ __device__ __forceinline__ void chain_op(const ChainArgs& a, COp& op, CTen* tens
       }
     }
   }
-  // the next op reads this op's LDS image / statistics and its global stores (workgroup-scope
-  // release / acquire)
+  chain_prm_store(a, smem, par ^ 1, pnext);
+  if (stamp && threadIdx.x == 0) stamp[3] = __builtin_amdgcn_s_memrealtime();
+  // the next op reads this op's LDS image / statistics / its parameters and its global stores
+  // (workgroup-scope release / acquire)
   __syncthreads();
 }
 
@@ -432,9 +466,20 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain_kernel(ChainArgs 
   const int t_now = a.t_dev ? *a.t_dev : 0;
   const int ng = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int trow = a.temb_per_b ? b : t_now;
+  int par = 0;                      // parameter buffer of the current conv op
+  {
+    int nx = 0;
+    while (nx < a.nops && ((COp*)a.ops)[nx].kind == 1) ++nx;
+    float v[kPrmPerThread];
+    chain_prm_load(a, (COp*)a.ops, nx, trow, v);
+    chain_prm_store(a, smem, 0, v);
+    __syncthreads();
+  }
   for (int i = 0; i < a.nops; ++i) {
     COp& op = ((COp*)a.ops)[i];
-    unsigned long long* stamp = a.stamps ? a.stamps + (size_t)b * 32 + 2 * min(i, 15) : nullptr;
+    int nx = i + 1;                 // the next conv op (its parameters are staged by this one)
+    while (nx < a.nops && ((COp*)a.ops)[nx].kind == 1) ++nx;
+    unsigned long long* stamp = a.stamps ? a.stamps + (size_t)b * 64 + 4 * min(i, 15) : nullptr;
     if (stamp && threadIdx.x == 0) stamp[0] = __builtin_amdgcn_s_memrealtime();
     if (op.kind == 1) {
       chain_reload<T>(op, (CTen*)a.tens, smem, b);
@@ -445,9 +490,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain_kernel(ChainArgs 
     // branch
 #define SDDM_CHAIN_OP(MFW, NFW)                                                                     \
   if (ng + kChainWaves * ((NFW) - 1) < (op.Cout >> 4))                                              \
-    chain_op<T, MFW, NFW, (MFW == 8 ? 1 : 2)>(a, op, (CTen*)a.tens, smem, b, trow, stamp);           \
+    chain_op<T, MFW, NFW, (MFW == 8 ? 1 : 2)>(a, op, (CTen*)a.tens, smem, b, trow, stamp, par, nx);  \
   else                                                                                            \
-    chain_op<T, MFW, (NFW) - 1, (MFW == 8 ? 1 : 2)>(a, op, (CTen*)a.tens, smem, b, trow, stamp);
+    chain_op<T, MFW, (NFW) - 1, (MFW == 8 ? 1 : 2)>(a, op, (CTen*)a.tens, smem, b, trow, stamp, par, nx);
     switch (op.var) {
       case 0: SDDM_CHAIN_OP(8, 2) break;
       case 1: SDDM_CHAIN_OP(8, 3) break;
@@ -455,8 +500,9 @@ __global__ __launch_bounds__(kChainThreads, 1) void conv_chain_kernel(ChainArgs 
       default: SDDM_CHAIN_OP(2, 3) break;
     }
 #undef SDDM_CHAIN_OP
+    par ^= 1;
   }
-  if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)b * 32 + 31] = __builtin_amdgcn_s_memrealtime();
+  if (a.stamps && threadIdx.x == 0) a.stamps[(size_t)b * 64 + 63] = __builtin_amdgcn_s_memrealtime();
 }
 
 }  // namespace

@@ -908,7 +908,9 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       }
       cp.cmax = cmax;
       cp.gsc = 0;
-      const int base = (8 * cmax + 255) / 256 * 256;
+      // [GN scale / shift 2 x cmax][two parameter buffers 3 x cmax] fp32 (conv_chain.hip)
+      const int base = (32 * cmax + 255) / 256 * 256;
+      if (3 * cmax > 4 * 256) ok = false;
       // residency: LDS segments per tensor (image uses in [t0, t1]); a segment after a gap in the
       // uses starts with a reload from the tensor's global copy when a res_conv operand needs it,
       // otherwise those uses read the global copy
@@ -1325,7 +1327,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
         SDDM_HIP_CHECK(hipMemset(c->stamp_buf, 0, sizeof(unsigned long long) * 8 * 65536));
         a.stamps = c->stamp_buf;
-        c->stamp_blocks = (int64_t)B * 4;
+        c->stamp_blocks = (int64_t)B * 8;
       }
       const std::string nm = "chain[" + cp.steps.front().w + ".." + cp.steps.back().w + "]";
       L.ops.push_back({2, bytes, flops, [ctx, lp, a, dt, B](hipStream_t s) {

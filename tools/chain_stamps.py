@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--N", type=int, default=16448)
     a = ap.parse_args()
     os.environ["SDDM_CHAIN_STAMPS"] = "1"
+    os.environ.setdefault("SDDM_CHAIN", "1")
     import numpy as np
     import torch
     import sddm_hip
@@ -48,15 +49,18 @@ def main():
     buf = np.zeros((65536, 8), dtype=np.uint64)
     n = ctypes.c_int64()
     sddm_hip.check(L.sddm_debug_stamps(ctx._h, buf.ctypes.data, 65536, ctypes.byref(n)))
-    st = buf[:n.value].reshape(a.batch, 32).astype(np.float64) * 0.01   # us
+    st = buf[:n.value].reshape(a.batch, 64).astype(np.float64) * 0.01   # us
     nops = int(os.environ.get("CHAIN_NOPS", "14"))
-    total = np.median(st[:, 31] - st[:, 0])
+    total = np.median(st[:, 63] - st[:, 0])
     print(f"chain total (median over images) {total:.1f} us")
+    print("  op: prologue (GN + first staging) | K loop | epilogue | to next op")
     for i in range(nops):
-        k = np.median(st[:, 2 * i + 1] - st[:, 2 * i]) if st[0, 2 * i + 1] > 0 else 0.0
-        nxt = st[:, 2 * i + 2] if i + 1 < nops else st[:, 31]
-        e = np.median(nxt - (st[:, 2 * i + 1] if st[0, 2 * i + 1] > 0 else st[:, 2 * i]))
-        print(f"  op {i:2d}: K loop {k:7.2f} us  epilogue/rest {e:6.2f} us")
+        s0, s1, s2, s3 = (st[:, 4 * i + k] for k in range(4))
+        nxt = st[:, 4 * i + 4] if i + 1 < nops else st[:, 63]
+        if s1[0] == 0:   # reload op
+            print(f"  op {i:2d}: reload {np.median(nxt - s0):6.2f} us")
+            continue
+        print(f"  op {i:2d}: {np.median(s1 - s0):6.2f} | {np.median(s2 - s1):7.2f} | {np.median(s3 - s2):6.2f} | {np.median(nxt - s3):5.2f}")
 
 
 if __name__ == "__main__":
