@@ -250,48 +250,51 @@ __device__ __forceinline__ void chain_op(const ChainArgs& a, COp& op, CTen* tens
     // between their addresses, and the closure would stay in scratch memory
     const int a_lds = A_lds, b_lds = B_lds, a_c = A_C, b_c = B_C, a_h = A_H, a_w = A_W, a_p = A_P;
     const T *a_g = A_g, *b_g = B_g;
-    for (int hb = 0; hb < HP; hb += NT) {
-      const int hp = hb + tid;
-      int hy, hx;
-      if (s2) {                     // polyphase plane ph = (row parity, column parity)
-        const int ph = fdivi(hp, rHPH), r2 = hp - ph * HPH, a2 = fdivi(r2, rHC);
-        hy = 2 * a2 + (ph >> 1);
-        hx = 2 * (r2 - a2 * HC) + (ph & 1);
-      } else {
-        hy = fdivi(hp, rHC);
-        hx = hp - hy * HC;
-      }
-      int iy = hy - 1, ix = hx - 1;
-      bool ok;
-      if (s2) ok = iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
-      else {
-        ok = iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
-        if (up) { iy >>= 1; ix >>= 1; }
-      }
-      ok = ok && hp < HP;
-      // LDS images are column-major (unit x * H + y), global tensors NHWC (pixel y * W + x)
-      const int lpx = ok ? ix * a_h + iy : 0, gpx = ok ? iy * a_w + ix : 0;
-      const int dst = stg + hp * 16;
-      for (int cc = 0; cc < k1 - k0; ++cc) {
+    // units (chunk, plane, halo pixel) flattened over all threads, halo pixels fastest: every wave
+    // takes a share even when the halo is smaller than the workgroup (the 8 x 4 levels)
+    const int cq_n = (k1 - k0) * 4, total = cq_n * HP;
+    const float rHP = 1.0f / (float)HP;
+    constexpr int SU = 4;           // units in flight per thread (loads first, then transforms)
+    for (int u0 = tid; u0 < total; u0 += SU * NT) {
+      f32x4 x[SU];
+      int dst[SU], ch[SU];
+#pragma unroll
+      for (int m = 0; m < SU; ++m) {
+        const int u = min(u0 + m * NT, total - 1);
+        const int cq = fdivi(u, rHP), hp = u - cq * HP, cc = cq >> 2, q = cq & 3;
+        int hy, hx;
+        if (s2) {                   // polyphase plane ph = (row parity, column parity)
+          const int ph = fdivi(hp, rHPH), r2 = hp - ph * HPH, a2 = fdivi(r2, rHC);
+          hy = 2 * a2 + (ph >> 1);
+          hx = 2 * (r2 - a2 * HC) + (ph & 1);
+        } else {
+          hy = fdivi(hp, rHC);
+          hx = hp - hy * HC;
+        }
+        int iy = hy - 1, ix = hx - 1;
+        bool ok;
+        if (s2) ok = iy >= 0 && iy < Hi && ix >= 0 && ix < Wi;
+        else {
+          ok = iy >= 0 && iy < Ho && ix >= 0 && ix < Wo;
+          if (up) { iy >>= 1; ix >>= 1; }
+        }
+        // LDS images are column-major (unit x * H + y), global tensors NHWC (pixel y * W + x)
+        const int lpx = ok ? ix * a_h + iy : 0, gpx = ok ? iy * a_w + ix : 0;
         const int c0 = (k0 + cc) * 32;
         const bool fa = c0 < CA;
         const int src_lds = fa ? a_lds : b_lds, src_c = fa ? a_c : b_c, cs = fa ? c0 : c0 - CA;
         const T* src_g = fa ? (const T*)a_g : (const T*)b_g;   // prvalues: no select of addresses
-        f32x4 v[4];
-        if (src_lds >= 0) {
+        if (src_lds >= 0) x[m] = *(const f32x4*)(smem + src_lds + (((cs >> 3) + q) * a_p + lpx) * 16);
+        else x[m] = gload16(src_g + ((size_t)b * a_p + gpx) * src_c + cs + q * 8);
+        dst[m] = u0 + m * NT < total ? stg + cc * SLOT + q * PLB + hp * 16 : -1;
+        ch[m] = ok ? c0 + q * 8 : -1;   // GN channel, -1: zero padding
+      }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = *(const f32x4*)(smem + src_lds + (((cs >> 3) + q) * a_p + lpx) * 16);
-        } else {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) v[q] = gload16(src_g + ((size_t)b * a_p + gpx) * src_c + cs + q * 8);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          f32x4 x = v[q];
-          if (gn) x = transform_lds<T>(x, gsc + c0 + q * 8, gsc + cmax + c0 + q * 8);
-          if (!ok) x = f32x4{0.f, 0.f, 0.f, 0.f};
-          if (hp < HP) *(f32x4*)(smem + dst + cc * SLOT + q * PLB) = x;
-        }
+      for (int m = 0; m < SU; ++m) {
+        f32x4 v = x[m];
+        if (gn) v = transform_lds<T>(v, gsc + max(ch[m], 0), gsc + cmax + max(ch[m], 0));
+        if (ch[m] < 0) v = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (dst[m] >= 0) *(f32x4*)(smem + dst[m]) = v;
       }
     }
   };
