@@ -22,4 +22,6 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 cp gpurun_out/prof_dw/run_kernel_stats.csv $O/${R}_diffwave_kernel_stats_T10_B64_bf16.csv
 timeout -k 10 900 python3 bench.py --workload wavegrad > $O/${R}_wavegrad_bench.json.log 2>&1 || { echo WG_FAIL; tail -5 $O/${R}_wavegrad_bench.json.log; exit 1; }
 tail -1 $O/${R}_wavegrad_bench.json.log | cut -c1-200
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_wg -o run -- python3 bench.py --workload wavegrad --timesteps 10 --steps 1 --warmup 1 --no-cpu-baseline > $O/${R}_wavegrad_T10_rocprof.json.log 2>&1 || { echo PROF_WG_FAIL; exit 1; }
+cp gpurun_out/prof_wg/run_kernel_stats.csv $O/${R}_wavegrad_kernel_stats_T10_B64_bf16.csv
 echo ALL_OK
