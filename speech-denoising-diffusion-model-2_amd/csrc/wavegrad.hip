@@ -67,6 +67,25 @@ __device__ __forceinline__ int wg_map(int t, int map, int f) {
   return map == WG_MAP_UP ? t / f : (map == WG_MAP_DOWN ? t * f : t);
 }
 
+// epilogue FiLM of the next conv's input (wavegrad.py:98-99, 104-105, 107-108): m = leaky(shift +
+// scale * v) for 4 channels at output element o; fp (shift) and fp + Cout (scale) at the same
+// position.  Moving the modulation here reads shift / scale once per element instead of once per
+// output-channel block of the consuming conv, and the consumer stages a plain input
+template <typename T>
+__device__ __forceinline__ void wg_film_epilogue(const WGConvArgs& a, const T* fp, size_t o, const float* v) {
+#pragma clang fp contract(off)
+  const f32x4 sh = load4<T>(fp), sc = load4<T>(fp + a.Cout);
+  float m[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) m[e] = wg_leaky(sh[e] + sc[e] * v[e]);
+  if (a.post_film == 2) {
+    store4<T>((T*)a.out + o, v[0], v[1], v[2], v[3]);
+    store4<T>((T*)a.out2 + o, m[0], m[1], m[2], m[3]);
+  } else {
+    store4<T>((T*)a.out + o, m[0], m[1], m[2], m[3]);
+  }
+}
+
 // B fragment at conv-input position tp (already bounds-checked by the caller via ok)
 template <typename T, int PRE>
 __device__ __forceinline__ Frag<T> wg_load_b(const WGConvArgs& a, const T* src_b, const T* film_b, int tp, bool ok,
@@ -174,7 +193,10 @@ __global__ __launch_bounds__(256) void wg_conv_kernel(WGConvArgs a) {
         for (int i = 0; i < 4; ++i)
           if (cb + i < a.Cout) o[cb + i] = v[i];
       } else if ((a.Cout & 3) == 0) {
-        if (cb < a.Cout) store4<T>((T*)a.out + ((size_t)b * Tc + t) * a.Cout + cb, v[0], v[1], v[2], v[3]);
+        const size_t o = ((size_t)b * Tc + t) * a.Cout + cb;
+        if (cb < a.Cout && a.post_film)
+          wg_film_epilogue<T>(a, (const T*)a.efilm + ((size_t)b * Tc + t) * 2 * a.Cout + cb, o, v);
+        else if (cb < a.Cout) store4<T>((T*)a.out + o, v[0], v[1], v[2], v[3]);
       } else {
         T* o = (T*)a.out + ((size_t)b * Tc + t) * a.Cout;
 #pragma unroll
@@ -311,27 +333,47 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
     enc = a.enc + (size_t)row * a.enc_stride + a.enc_off;
   }
   const T* res_b = a.res ? (const T*)a.res + (size_t)b * a.res_T * a.Cout : nullptr;
+  const T* ef_b = a.post_film ? (const T*)a.efilm + (size_t)b * Tc * 2 * a.Cout : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int cb = cob + wc + i * 16 + 4 * g;
     float bias[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[e] = a.bias[cb + e];
+    // the residual and FiLM operands of the 4 position tiles are loaded together (clamped
+    // positions), so a channel group waits on memory once rather than once per tile
+    typedef T vec4 __attribute__((ext_vector_type(4)));
+    vec4 rv[4], sh[4], sc[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int tcl = min(t0 + wt + p * 16 + l16, Tc - 1);
+      if (res_b) rv[p] = *(const vec4*)(res_b + (size_t)wg_map(tcl, a.res_map, a.res_f) * a.Cout + cb);
+      if (ef_b) {
+        sh[p] = *(const vec4*)(ef_b + (size_t)tcl * 2 * a.Cout + cb);
+        sc[p] = *(const vec4*)(ef_b + (size_t)tcl * 2 * a.Cout + a.Cout + cb);
+      }
+    }
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int t = t0 + wt + p * 16 + l16;
       if (t >= Tc) continue;
       float v[4];
-      f32x4 rv = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (res_b) rv = load4<T>(res_b + (size_t)wg_map(t, a.res_map, a.res_f) * a.Cout + cb);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float x = acc[i][p][e] + bias[e];
         if (a.post == 1) x = wg_leaky(x) + enc[cb + e];
-        if (res_b) x = x + rv[e];
+        if (res_b) x = x + to_f32<T>(rv[p][e]);
         v[e] = x;
       }
-      store4<T>((T*)a.out + ((size_t)b * Tc + t) * a.Cout + cb, v[0], v[1], v[2], v[3]);
+      const size_t o = ((size_t)b * Tc + t) * a.Cout + cb;
+      if (ef_b) {
+        float m[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) m[e] = wg_leaky(to_f32<T>(sh[p][e]) + to_f32<T>(sc[p][e]) * v[e]);
+        if (a.post_film == 2) store4<T>((T*)a.out2 + o, m[0], m[1], m[2], m[3]);
+        else { v[0] = m[0]; v[1] = m[1]; v[2] = m[2]; v[3] = m[3]; }
+      }
+      store4<T>((T*)a.out + o, v[0], v[1], v[2], v[3]);
     }
   }
 }
@@ -423,6 +465,8 @@ hipError_t launch_wg_conv(int dtype, const WGConvArgs& a, hipStream_t s) {
     return hipErrorInvalidValue;
   if ((a.map == WG_MAP_UP && (a.f < 1 || a.src_T * a.f != a.Tc)) || (a.map == WG_MAP_DOWN && a.src_T / a.f != a.Tc) ||
       (a.map == WG_MAP_ID && a.src_T != a.Tc) || (a.pre == 2 && !a.film) || (a.post == 1 && (!a.enc || (!a.enc_per_b && !a.t_dev))))
+    return hipErrorInvalidValue;
+  if (a.post_film && (a.post_film > 2 || !a.efilm || a.out_f32 || a.Cout % 4 || (a.post_film == 2 && !a.out2)))
     return hipErrorInvalidValue;
   if (a.res && ((a.res_map == WG_MAP_UP && a.res_T * a.res_f != a.Tc) || (a.res_map == WG_MAP_ID && a.res_T != a.Tc)))
     return hipErrorInvalidValue;

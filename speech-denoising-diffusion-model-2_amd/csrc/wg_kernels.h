@@ -22,6 +22,10 @@ struct WGConvArgs {
   const void* res; int res_map, res_f, res_T;  // [B][res_T][Cout] (T) or null
   void* out; int out_f32;                      // [B][Tc][Cout] (T, or fp32 when out_f32)
   int B;
+  // FiLM of the NEXT conv's input applied in this conv's epilogue (16-bit / fp32 storage, Cout % 4
+  // == 0): m = leaky(shift + scale * v) with efilm [B][Tc][2 Cout] (shift | scale).  post_film 1:
+  // out <- m (v is consumed only through the FiLM); 2: out <- v and out2 <- m (v is also a residual)
+  const void* efilm; void* out2; int post_film;
 };
 hipError_t launch_wg_conv(int dtype, const WGConvArgs& a, hipStream_t s);
 // true when launch_wg_conv takes the LDS-staged kernel (which applies pre == 2 itself)

@@ -156,7 +156,7 @@ static int wg_prepare(sddm_ctx* c, int B, int F) {
     const std::string s = std::to_string(i);
     const int64_t lin = L[5 - i], lout = L[4 - i];
     buf("u" + s + "b1", lin, wg::kUp[i].h);
-    for (const char* n : {"y0", "x", "z", "", "m"}) buf("u" + s + n, lout, wg::kUp[i].h);   // m: FiLM-modulated input
+    for (const char* n : {"y0", "x", "z", "", "m", "p"}) buf("u" + s + n, lout, wg::kUp[i].h);   // m: leaky(film(x)); p: pre-2 fallback scratch
   }
   d.aoff["eps"] = A.reserve(sizeof(float) * (size_t)B * L[0]);
   d.aoff["encb"] = A.reserve(sizeof(float) * (size_t)B * WGState::kEncN);
@@ -171,6 +171,7 @@ struct WGConvSpec {
   std::string w; int Cout, K, dil, pre; const char* film;
   int post, enc_off; const char* res; int res_map, res_f; int64_t res_T;
   const char* out;
+  const char* efilm = nullptr; int post_film = 0; const char* out2 = nullptr;   // WGConvArgs::post_film
 };
 
 static int wg_conv(sddm_ctx* c, WGConvSpec q, int B, const float* enc, int enc_per_b, const int* t_dev,
@@ -181,7 +182,7 @@ static int wg_conv(sddm_ctx* c, WGConvSpec q, int B, const float* enc, int enc_p
   WGConvArgs probe{};
   probe.Cout = q.Cout; probe.K = q.K; probe.dil = q.dil; probe.pre = q.pre; probe.out_f32 = 0;
   if (q.pre == 2 && !wg_conv_uses_lds(probe)) {   // modulate once into the UBlock's scratch, then a plain conv
-    mod = std::string(q.out).substr(0, 2) + "m";
+    mod = std::string(q.out).substr(0, 2) + "p";
     WGFilmArgs fa{d.act.base + d.aoff.at(q.src), d.act.base + d.aoff.at(q.film), d.act.base + d.aoff.at(mod),
                   (int64_t)B * q.Tc, q.Cin};
     SDDM_HIP_CHECK(launch_wg_film(c->dtype, fa, s));
@@ -200,6 +201,9 @@ static int wg_conv(sddm_ctx* c, WGConvSpec q, int B, const float* enc, int enc_p
   a.res_T = (int)q.res_T;
   a.out = d.act.base + d.aoff.at(q.out); a.out_f32 = std::strcmp(q.out, "eps") == 0;
   a.B = B;
+  a.post_film = q.post_film;
+  a.efilm = q.efilm ? d.act.base + d.aoff.at(q.efilm) : nullptr;
+  a.out2 = q.out2 ? d.act.base + d.aoff.at(q.out2) : nullptr;
   const hipError_t e = launch_wg_conv(c->dtype, a, s);
   if (e != hipSuccess) FAIL(SDDM_ERR_HIP, "wg_conv %s: %s", q.w.c_str(), hipGetErrorString(e));
   return SDDM_OK;
@@ -270,18 +274,31 @@ static int wg_network(sddm_ctx* c, const float* audio, int B, int F, const float
     const std::string si = std::to_string(i), p = "upsample." + si + ".", o = "u" + si;
     const std::string film = "f" + std::to_string(4 - i);
     const int64_t lin = L[5 - i], lout = L[4 - i];
+    // FiLM placement.  512-channel UBlocks (upsample.0-1): the FiLM of block2.1 / block3.0 /
+    // block3.1's inputs runs in their producers' epilogues (post_film: y0 holds leaky(film(block2.0
+    // out)), m holds leaky(film(x)), z holds leaky(film(block3.0 out))), so shift / scale are read
+    // once per element instead of once per 128-channel block of the consumer (upsample.1: 1137 ->
+    // 962 us per step at B=64).  upsample.0's block2.0 is step-invariant (wg_condition), so its
+    // block2.1 keeps the FiLM in the staging (pre 2).  The 128 / 256-channel UBlocks keep the
+    // staged FiLM: there the epilogue loads are exposed (all blocks reach their epilogues
+    // together) and cost more than the re-reads save (upsample.4: 1324 -> 1675 us)
+    const std::string ym = o + "y0", xm = o + "m", xo = o + "x", zo = o + "z", b1 = o + "b1";
+    const bool epi = u.h >= 512;
     if (i > 0) {
       WG_TRY(wg_conv(c, {x.c_str(), lin, u.ci, WG_MAP_ID, 1, lin, u.ci, p + "block1", u.h, 1, 1, 0, nullptr, 0, 0, nullptr, 0, 1, 0,
-                         (o + "b1").c_str()}, B, enc, enc_per_b, t_dev, s));
+                         b1.c_str()}, B, enc, enc_per_b, t_dev, s));
       WG_TRY(wg_conv(c, {x.c_str(), lin, u.ci, WG_MAP_UP, u.f, lout, u.ci, p + "block2.0", u.h, 3, u.dil[0], 1, nullptr, 0, 0,
-                         nullptr, 0, 1, 0, (o + "y0").c_str()}, B, enc, enc_per_b, t_dev, s));
+                         nullptr, 0, 1, 0, ym.c_str(), epi ? film.c_str() : nullptr, epi ? 1 : 0}, B, enc, enc_per_b, t_dev, s));
     }
-    WG_TRY(wg_conv(c, {(o + "y0").c_str(), lout, u.h, WG_MAP_ID, 1, lout, u.h, p + "block2.1", u.h, 3, u.dil[1], 2, film.c_str(),
-                       0, 0, (o + "b1").c_str(), WG_MAP_UP, u.f, lin, (o + "x").c_str()}, B, enc, enc_per_b, t_dev, s));
-    WG_TRY(wg_conv(c, {(o + "x").c_str(), lout, u.h, WG_MAP_ID, 1, lout, u.h, p + "block3.0", u.h, 3, u.dil[2], 2, film.c_str(),
-                       0, 0, nullptr, 0, 1, 0, (o + "z").c_str()}, B, enc, enc_per_b, t_dev, s));
-    WG_TRY(wg_conv(c, {(o + "z").c_str(), lout, u.h, WG_MAP_ID, 1, lout, u.h, p + "block3.1", u.h, 3, u.dil[3], 2, film.c_str(),
-                       0, 0, (o + "x").c_str(), WG_MAP_ID, 1, lout, o.c_str()}, B, enc, enc_per_b, t_dev, s));
+    const bool pre21 = !epi || i == 0;
+    WG_TRY(wg_conv(c, {ym.c_str(), lout, u.h, WG_MAP_ID, 1, lout, u.h, p + "block2.1", u.h, 3, u.dil[1], pre21 ? 2 : 0,
+                       pre21 ? film.c_str() : nullptr, 0, 0, b1.c_str(), WG_MAP_UP, u.f, lin, xo.c_str(),
+                       epi ? film.c_str() : nullptr, epi ? 2 : 0, epi ? xm.c_str() : nullptr}, B, enc, enc_per_b, t_dev, s));
+    WG_TRY(wg_conv(c, {epi ? xm.c_str() : xo.c_str(), lout, u.h, WG_MAP_ID, 1, lout, u.h, p + "block3.0", u.h, 3, u.dil[2],
+                       epi ? 0 : 2, epi ? nullptr : film.c_str(), 0, 0, nullptr, 0, 1, 0, zo.c_str(), epi ? film.c_str() : nullptr,
+                       epi ? 1 : 0}, B, enc, enc_per_b, t_dev, s));
+    WG_TRY(wg_conv(c, {zo.c_str(), lout, u.h, WG_MAP_ID, 1, lout, u.h, p + "block3.1", u.h, 3, u.dil[3], epi ? 0 : 2,
+                       epi ? nullptr : film.c_str(), 0, 0, xo.c_str(), WG_MAP_ID, 1, lout, o.c_str()}, B, enc, enc_per_b, t_dev, s));
     x = o;
   }
   WG_TRY(wg_conv(c, {x.c_str(), L[0], 128, WG_MAP_ID, 1, L[0], 128, "last_conv", 1, 3, 1, 0, nullptr, 0, 0, nullptr, 0, 1, 0, "eps"},
