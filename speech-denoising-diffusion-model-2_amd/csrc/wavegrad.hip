@@ -334,23 +334,39 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
   }
   const T* res_b = a.res ? (const T*)a.res + (size_t)b * a.res_T * a.Cout : nullptr;
   const T* ef_b = a.post_film ? (const T*)a.efilm + (size_t)b * Tc * 2 * a.Cout : nullptr;
+  // FiLM operands (shift, scale) of the epilogue: 16-bit storage loads all 16 tiles' at once (64
+  // VGPRs, free once the K loop is done), so a block waits on them once; fp32 loads them per
+  // channel group.  Positions are clamped (rows past Tc are not stored)
+  typedef T vec4 __attribute__((ext_vector_type(4)));
+  constexpr int GI = sizeof(T) == 2 ? 4 : 1;
+  vec4 sh[GI][4], sc[GI][4];
+  if (GI == 4 && ef_b) {
+#pragma unroll
+    for (int i = 0; i < GI; ++i)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) {
+        const T* fp = ef_b + (size_t)min(t0 + wt + p * 16 + l16, Tc - 1) * 2 * a.Cout + cob + wc + i * 16 + 4 * g;
+        sh[i][p] = *(const vec4*)fp;
+        sc[i][p] = *(const vec4*)(fp + a.Cout);
+      }
+  }
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int cb = cob + wc + i * 16 + 4 * g;
+    const int fi = GI == 4 ? i : 0;
     float bias[4];
 #pragma unroll
     for (int e = 0; e < 4; ++e) bias[e] = a.bias[cb + e];
-    // the residual and FiLM operands of the 4 position tiles are loaded together (clamped
-    // positions), so a channel group waits on memory once rather than once per tile
-    typedef T vec4 __attribute__((ext_vector_type(4)));
-    vec4 rv[4], sh[4], sc[4];
+    // the residual operands of the 4 position tiles are loaded together, so a channel group waits
+    // on memory once rather than once per tile
+    vec4 rv[4];
 #pragma unroll
     for (int p = 0; p < 4; ++p) {
       const int tcl = min(t0 + wt + p * 16 + l16, Tc - 1);
       if (res_b) rv[p] = *(const vec4*)(res_b + (size_t)wg_map(tcl, a.res_map, a.res_f) * a.Cout + cb);
-      if (ef_b) {
-        sh[p] = *(const vec4*)(ef_b + (size_t)tcl * 2 * a.Cout + cb);
-        sc[p] = *(const vec4*)(ef_b + (size_t)tcl * 2 * a.Cout + a.Cout + cb);
+      if (GI == 1 && ef_b) {
+        sh[0][p] = *(const vec4*)(ef_b + (size_t)tcl * 2 * a.Cout + cb);
+        sc[0][p] = *(const vec4*)(ef_b + (size_t)tcl * 2 * a.Cout + a.Cout + cb);
       }
     }
 #pragma unroll
@@ -369,7 +385,7 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
       if (ef_b) {
         float m[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) m[e] = wg_leaky(to_f32<T>(sh[p][e]) + to_f32<T>(sc[p][e]) * v[e]);
+        for (int e = 0; e < 4; ++e) m[e] = wg_leaky(to_f32<T>(sh[fi][p][e]) + to_f32<T>(sc[fi][p][e]) * v[e]);
         if (a.post_film == 2) store4<T>((T*)a.out2 + o, m[0], m[1], m[2], m[3]);
         else { v[0] = m[0]; v[1] = m[1]; v[2] = m[2]; v[3] = m[3]; }
       }

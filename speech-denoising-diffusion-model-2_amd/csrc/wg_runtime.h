@@ -283,7 +283,8 @@ static int wg_network(sddm_ctx* c, const float* audio, int B, int F, const float
     // staged FiLM: there the epilogue loads are exposed (all blocks reach their epilogues
     // together) and cost more than the re-reads save (upsample.4: 1324 -> 1675 us)
     const std::string ym = o + "y0", xm = o + "m", xo = o + "x", zo = o + "z", b1 = o + "b1";
-    const bool epi = u.h >= 512;
+    static const int epi_min_h = std::getenv("SDDM_WG_EPI_MIN_H") ? std::atoi(std::getenv("SDDM_WG_EPI_MIN_H")) : 512;
+    const bool epi = u.h >= epi_min_h;
     if (i > 0) {
       WG_TRY(wg_conv(c, {x.c_str(), lin, u.ci, WG_MAP_ID, 1, lin, u.ci, p + "block1", u.h, 1, 1, 0, nullptr, 0, 0, nullptr, 0, 1, 0,
                          b1.c_str()}, B, enc, enc_per_b, t_dev, s));
