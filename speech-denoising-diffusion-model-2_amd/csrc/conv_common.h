@@ -141,7 +141,22 @@ struct GNFuse {
   int G; float eps;
 };
 
-__device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
+// Loads of bytes another workgroup of the same launch stored (HO, conv_deep.hip's team kernel):
+// buffer loads with sc1 over a resource based at the lane arena `hb` (every activation and
+// statistics tensor lies in it, < 4 GiB), served by the XCD's L2 past this CU's L1.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t ho_rsrc(const char* hb) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)hb, (short)0, -1, 0x00020000);
+}
+template <bool HO = false>
+__device__ __forceinline__ float ld_stat(const float* p, const char* hb) {
+  if constexpr (HO)
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ho_rsrc(hb), (unsigned)((const char*)p - hb), 0, 16));
+  else return *p;
+}
+
+template <bool HO = false>
+__device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh,
+                                                  const char* hb = nullptr) {
   const int C = CA + CB, cpg = C / f.G;
   const int tpg = pow2_floor(blockDim.x / f.G);   // threads per group (power of two, <= 64)
   const int g = threadIdx.x / tpg, sub = threadIdx.x - g * tpg;
@@ -158,7 +173,7 @@ __device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA
   double s = 0.0;
   for (int i = sub; i < items; i += tpg) {
     const int c = i / tiles, t = i - c * tiles;
-    s += (double)base[((size_t)t * Cs + cs0 + c) * 2];
+    s += (double)ld_stat<HO>(base + ((size_t)t * Cs + cs0 + c) * 2, hb);
   }
   for (int o = 1; o < tpg; o <<= 1) s += __shfl_xor(s, o);
   const double n_tot = (double)items * ntile;
@@ -167,8 +182,8 @@ __device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA
   for (int i = sub; i < items; i += tpg) {
     const int c = i / tiles, t = i - c * tiles;
     const float* e = base + ((size_t)t * Cs + cs0 + c) * 2;
-    const double d = (double)e[0] / ntile - mean;
-    m2 += (double)e[1] + (double)ntile * d * d;
+    const double d = (double)ld_stat<HO>(e, hb) / ntile - mean;
+    m2 += (double)ld_stat<HO>(e + 1, hb) + (double)ntile * d * d;
   }
   for (int o = 1; o < tpg; o <<= 1) m2 += __shfl_xor(m2, o);
   const double rstd = 1.0 / sqrt(m2 / n_tot + (double)f.eps);
@@ -241,7 +256,9 @@ struct GNLoad {
   // readable address): the kernels call issue() unconditionally, because a load inside a branch
   // makes the compiler wait for it at the branch join, serialising this round trip in front of
   // every other load of the prologue.
-  __device__ __forceinline__ void issue(const GNFuse& f, int b, int CA, int CB, bool on, const float* safe) {
+  template <bool HO = false>
+  __device__ __forceinline__ void issue(const GNFuse& f, int b, int CA, int CB, bool on, const float* safe,
+                                        const char* hb = nullptr) {
     const int G = f.G > 0 ? f.G : 32;
     const int C = CA + CB, cpg = C / G;
     tpg = pow2_floor(blockDim.x / G);                 // xor butterflies: a power of two (6-wave blocks)
@@ -266,16 +283,23 @@ struct GNLoad {
       const int i = min(sub + k * tpg, items - 1);
       const int c = fdivi(i, rt), t = i - c * tiles;
       const int off = on ? (t * Cs + cs0 + c) * 2 : 0;   // 32-bit offsets: no 64-bit address math
-      v[k] = *(const float2*)(base + off);
+      if constexpr (HO) {
+        const unsigned long long u = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_raw_buffer_load_b64(
+            ho_rsrc(hb), (unsigned)((const char*)(base + off) - hb), 0, 16));
+        v[k] = make_float2(__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)));
+      }
+      else v[k] = *(const float2*)(base + off);
     }
     const int cg = on ? c0 + min(sub, cpg - 1) : 0;   // clamped: unconditional loads
     gm = (on ? f.gamma : safe)[cg];
     bt = (on ? f.beta : safe)[cg];
   }
 
-  __device__ __forceinline__ void finish(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
+  template <bool HO = false>
+  __device__ __forceinline__ void finish(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh,
+                                         const char* hb = nullptr) {
     if (!fast) {
-      gn_fused_prologue(f, b, CA, CB, sc, sh);
+      gn_fused_prologue<HO>(f, b, CA, CB, sc, sh, hb);
       return;
     }
     if (grp >= f.G) return;

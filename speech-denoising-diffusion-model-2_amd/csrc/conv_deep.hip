@@ -74,8 +74,32 @@ __device__ __forceinline__ void chan_merge(float& n, float& mean, float& m2, flo
   n = nt;
 }
 
-template <typename T, bool S2, int MT, int NW, int D, int NB>
-__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) {
+// Activation loads.  HO (hand-off mode, the team kernel below): the bytes were stored by another
+// workgroup of this launch on the same XCD, so they are read from that XCD's L2 past this CU's L1
+// (which may still hold stale lines of the same addresses): buffer_load ... sc1 over the lane
+// arena `hb` (conv_common.h ho_rsrc).
+template <bool HO>
+__device__ __forceinline__ f32x4 ld_act(const f32x4* p, const char* hb) {
+  if constexpr (HO)
+    return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(ho_rsrc(hb), (unsigned)((const char*)p - hb), 0, 16));
+  else return *p;
+}
+
+struct NoWait {
+  __device__ __forceinline__ void operator()() const {}
+};
+
+// The noise-embedding row of a conv (ResnetBlock.noise_func): table [rows][ld], the row is the
+// step counter *t_dev (sampling) or the image (network forward, per_b); tab == null: none
+struct TembRef { const float* tab; int ld; const int* t_dev; int per_b; };
+
+// One output tile (TR x TW pixels of image b, output channels [zb NB, zb NB + NB)) of the
+// whole-K-resident convolution.  `wait` runs after the weight fragments are issued and before
+// any activation is loaded (team kernel: the dependency poll; per-layer kernel: nothing).
+template <typename T, bool S2, int MT, int NW, int D, int NB, bool HO, typename Wait>
+__device__ __forceinline__ void deep_tile(const ConvArgs& a, const TembRef& te, int tile, int b, int zb, char* smem,
+                                          const Wait& wait, const char* hb = nullptr,
+                                          unsigned long long* hst = nullptr) {
   constexpr int NT = 64 * NW;
   constexpr int ES = (int)sizeof(T);
   constexpr int UPP = 2 * ES;          // 16-byte planes per 32-channel chunk
@@ -87,12 +111,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   static_assert(NB == 16 || NB == 32, "16 or 32 output channels per block");
   constexpr int MAXU = ES == 4 ? (NW == 8 ? 6 : 8) : (NW == 8 ? 10 : 16);   // units per thread per pass
   constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  int tid = threadIdx.x;
+  // team kernel: an opaque copy per item, so the per-thread index math of the staging units is
+  // recomputed inside the ticket loop instead of being hoisted out of it and kept live (spilled)
+  if constexpr (HO) asm volatile("" : "+v"(tid));
+  const int lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
-  int tile, b, zb;
-  xcd_block(a.n_tiles, a.Cout / NB, tile, b, zb);
   const int n0 = zb * NB;
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int y0 = ty * a.TR, x0 = tx * a.TW;
@@ -113,10 +138,40 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   const T* rsrc = ident ? (const T*)a.res_src + (size_t)b * img_out * a.Cout + n0 : srcA;
   SDDM_STAMP(a, 0);
 
+  // this wave's K steps (wave-uniform) and the first D weight fragments of each
+  const int ns3 = nck * 9, ns = ns3 + rck;
+  const int nj = wv < ns ? (ns - wv + NW - 1) / NW : 0;
+  const int s_last = wv + NW * max(nj - 1, 0);
+  // weights in MFMA-fragment order (ConvArgs::wgt_f): the 64 lanes of one A fragment read one
+  // contiguous 1 KiB (bf16 / f16) or 2 KiB (fp32) run, not 16 rows x 64 B pieces
+  const int cb0 = n0 / 16;
+  const T* wbase = (const T*)a.wgt_f + (size_t)lane * 8;
+  const T* rbase = (const T*)a.res_wgt_f + (size_t)lane * 8;
+  auto wfrag = [&](int s, int fc) -> Frag<T> {
+    const T* p = s < ns3 ? wbase + ((size_t)(cb0 + fc) * ns3 + s) * 512
+                         : rbase + ((size_t)(cb0 + fc) * rck + (s - ns3)) * 512;
+    return load_frag<T>((const char*)p);
+  };
+  Frag<T> wa[D][FC];
+  auto issue_weights = [&]() {
+#pragma unroll
+    for (int d = 0; d < D; ++d)
+#ifdef SDDM_DEEP_GUARD
+      if (d < nj)                                        // wave-uniform
+#endif
+      {
+#pragma unroll
+        for (int fc = 0; fc < FC; ++fc) wa[d][fc] = (a.dbg & 32) ? Frag<T>{} : wfrag(min(wv + NW * d, s_last), fc);
+      }
+  };
+  // hand-off mode: the weights (never written in the launch) stream in while the dependency is awaited
+  if constexpr (HO) issue_weights();
+  wait();
+
   // ---------------- 1. issue every load of the block ----------------
   GNLoad gl;
   const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
+  gl.template issue<HO>(gf, b, a.CA, a.CB, gn, a.bias, hb);
 
   // staging units: [0, n3) halo planes (8 lanes = 8 consecutive halo pixels of one plane),
   // [n3, n3 + nres) raw res_conv input at the output pixels, then the identity-residual tile
@@ -170,7 +225,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
         gs = -1;
       }
     }
-    r = *(const f32x4*)ptr;
+    r = ld_act<HO>((const f32x4*)ptr, hb);
     pk = d < 0 ? -1 : (d << 10) | (gs + 2);
   };
   auto commit = [&](const f32x4& r, int pk) {
@@ -197,36 +252,13 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 
   // the step counter selecting the noise-embedding row (loaded with everything else; the
   // bias + embedding loads that depend on it are issued after the staging wait)
-  const int t_now = a.t_dev ? *a.t_dev : 0;
+  const int t_now = te.t_dev ? *te.t_dev : 0;
 
-  // this wave's K steps (wave-uniform) and the first D weight fragments of each
-  const int ns3 = nck * 9, ns = ns3 + rck;
-  const int nj = wv < ns ? (ns - wv + NW - 1) / NW : 0;
-  const int s_last = wv + NW * max(nj - 1, 0);
-  // weights in MFMA-fragment order (ConvArgs::wgt_f): the 64 lanes of one A fragment read one
-  // contiguous 1 KiB (bf16 / f16) or 2 KiB (fp32) run, not 16 rows x 64 B pieces
-  const int cb0 = n0 / 16;
-  const T* wbase = (const T*)a.wgt_f + (size_t)lane * 8;
-  const T* rbase = (const T*)a.res_wgt_f + (size_t)lane * 8;
-  auto wfrag = [&](int s, int fc) -> Frag<T> {
-    const T* p = s < ns3 ? wbase + ((size_t)(cb0 + fc) * ns3 + s) * 512
-                         : rbase + ((size_t)(cb0 + fc) * rck + (s - ns3)) * 512;
-    return load_frag<T>((const char*)p);
-  };
-  Frag<T> wa[D][FC];
-#pragma unroll
-  for (int d = 0; d < D; ++d)
-#ifdef SDDM_DEEP_GUARD
-    if (d < nj)                                          // wave-uniform
-#endif
-    {
-#pragma unroll
-      for (int fc = 0; fc < FC; ++fc) wa[d][fc] = (a.dbg & 32) ? Frag<T>{} : wfrag(min(wv + NW * d, s_last), fc);
-    }
+  if constexpr (!HO) issue_weights();
   SDDM_STAMP(a, 1);
 
   // ---------------- 2. GroupNorm finalize, GN + SiLU into the LDS image ----------------
-  if (gn && !(a.dbg & 1)) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
+  if (gn && !(a.dbg & 1)) gl.template finish<HO>(gf, b, a.CA, a.CB, gsc, gsc + Cin, hb);
   lds_sync();                                            // scale / shift visible (loads stay in flight)
   SDDM_STAMP(a, 2);
 #pragma unroll
@@ -243,19 +275,20 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   }
   lds_sync();
   SDDM_STAMP(a, 3);
+  if (HO && hst && wv == 0) hst[0] = __builtin_amdgcn_s_memrealtime();   // team stamps (experiments)
   // bias + noise embedding of this thread's 4 epilogue channels: in flight during the K loop
   const int ec4 = (tid & (TPP - 1)) * 4;
   float bb[4], sshift;
   {
-    const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
+    const float* trow = te.tab ? te.tab + (size_t)(te.per_b ? b : t_now) * te.ld : a.bias;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {                        // unconditional loads (no wait at a join)
       const float bv = a.bias[n0 + ec4 + i], tv = trow[n0 + ec4 + i];
-      bb[i] = bv + (a.temb ? tv : 0.f);
+      bb[i] = bv + (te.tab ? tv : 0.f);
     }
     const int cs = n0 + (tid & (NB - 1));                // statistics shift of channel n0 + tid (tid < NB)
     const float sbv = a.bias[cs], stv = trow[cs];
-    sshift = sbv + (a.temb ? stv : 0.f);
+    sshift = sbv + (te.tab ? stv : 0.f);
   }
 
   // ---------------- 3. this wave's K steps ----------------
@@ -303,6 +336,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
     }
   }
   SDDM_STAMP(a, 4);
+  if (HO && hst && wv == 0) hst[1] = __builtin_amdgcn_s_memrealtime();
 
   // ---------------- 4. reduce the partial tiles: red[slot][MT][NBP] ----------------
   lds_sync();                                       // every wave is done with the image
@@ -364,6 +398,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
     }
   }
   SDDM_STAMP(a, 5);
+  if (HO && hst && wv == 0) hst[2] = __builtin_amdgcn_s_memrealtime();
   if (a.stats && !(a.dbg & 16)) {
     // the lanes of a DPP row holding the same 4 channels (16 / TPP of them, TPP apart) add by
     // row rotations, then the 4 rows of every wave through LDS, summed by one thread per channel
@@ -398,7 +433,128 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
     }
   }
   SDDM_STAMP(a, 6);
+  if (HO && hst && wv == 0) hst[3] = __builtin_amdgcn_s_memrealtime();
   SDDM_STAMP(a, 7);
+}
+
+// One launch per layer: one tile per block, in the XCD-aware block order.
+template <typename T, bool S2, int MT, int NW, int D, int NB>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int tile, b, zb;
+  xcd_block(a.n_tiles, a.Cout / NB, tile, b, zb);
+  const TembRef te{a.temb, a.temb_ld, a.t_dev, a.temb_per_b};
+  deep_tile<T, S2, MT, NW, D, NB, false>(a, te, tile, b, zb, smem, NoWait{});
+}
+
+// ---------------------------------------------------------------------------------------------
+// Deep-level team kernel: a run of consecutive convolutions (the UNet levels whose images are a
+// few hundred pixels: Downsample -> ResnetBlocks -> mid -> ResnetBlocks -> Upsample, the loop
+// bodies of UNetModified2.py:252-265) as ONE launch.  Per-layer launches of these layers are
+// each a chain of dependent memory round trips after a kernel boundary (L2 written back and
+// invalidated, HBM latency for every first load); here the images never leave the L2 of the XCD
+// that works on them:
+//   * image b belongs to the team of XCD b % 8; a workgroup reads its XCD from HW_REG_XCC_ID and
+//     serves that team, so producer and consumer of every hand-off share one L2 whatever the
+//     dispatcher's placement;
+//   * a team's work is a ticket queue in op-major order (op, image, tile x channel block); a
+//     workgroup takes the next ticket, issues the item's weight fragments (constant in the
+//     launch), then polls the per-(op, image) completion counter of the op it reads from, reads
+//     the activations, GroupNorm statistics and residuals past its L1 (ld_act<true>) and computes
+//     exactly the per-layer kernel's tile (same tiling, same arithmetic: bit-identical outputs);
+//   * completion: every wave drains its stores (s_waitcnt vmcnt(0): the stores reached the L2),
+//     workgroup barrier, one lane adds 1 to the counter (an L2 atomic of this XCD).
+// Tickets are taken in dependency order, so the lowest unfinished ticket never waits on an
+// unclaimed one: no co-residency is assumed and the queue cannot deadlock.  Spins are bounded
+// (s_memrealtime); a timeout sets the error word and the workgroup carries on.
+// ---------------------------------------------------------------------------------------------
+// variant index: s2 * 6 + mt_index(32, 64, 128) * 2 + (nb == 32)
+__host__ __device__ constexpr int team_var(bool s2, int mt, int nb) {
+  return (s2 ? 6 : 0) + (mt == 32 ? 0 : mt == 64 ? 1 : 2) * 2 + (nb == 32 ? 1 : 0);
+}
+
+template <typename T>
+__global__ __launch_bounds__(256, 2) void conv_team_kernel(TeamArgs ta, const TeamOp* __restrict__ ops) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  __shared__ int s_ticket;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc));
+  xcc &= 7;
+  const int B = ta.B;
+  const int nimg = (int)xcc < B ? (B - 1 - (int)xcc) / 8 + 1 : 0;
+  if (nimg == 0) return;
+  unsigned* ticket = ta.ctr + xcc * 32;                  // one 128-byte line per team
+  unsigned* done = ta.ctr + 8 * 32;                      // [nops][B]
+  // Only wave-uniform branches around the barriers of this loop: a lane-0 branch (ticket, poll,
+  // publish) gets structurised into a lane-divergent loop around the barriers, which hangs (measured).
+  // Wave 0 takes the ticket (its lane 0 adds 1), polls and publishes.
+  const bool w0 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) == 0;
+  const unsigned one = (threadIdx.x & 63) == 0 ? 1u : 0u;
+  for (;;) {
+    if (w0)
+      s_ticket = (int)__builtin_amdgcn_readfirstlane(
+          __hip_atomic_fetch_add(ticket, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    __syncthreads();
+    int t = __builtin_amdgcn_readfirstlane(s_ticket);   // uniform: the op table is read through SGPRs
+    const int tk = t;
+    unsigned long long* hst = ta.stamps && tk < 4096 ? ta.stamps + ((size_t)xcc * 4096 + tk) * 8 + 4 : nullptr;
+    const unsigned long long ts0 = ta.stamps ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    unsigned long long ts1 = 0;
+    int op = 0;
+    for (; op < ta.nops; ++op) {                         // scalar walk over the op table
+      const int n = nimg * ops[op].items;
+      if (t < n) break;
+      t -= n;
+    }
+    if (op >= ta.nops) break;
+    const TeamOp& o = ops[op];
+    const int j = t / o.items, item = t - j * o.items;
+    const int b = (int)xcc + 8 * j;
+    const int zb = item / o.a.n_tiles, tile = item - zb * o.a.n_tiles;
+    const TembRef te{o.toff >= 0 ? ta.temb + o.toff : nullptr, ta.temb_ld, ta.t_dev, ta.temb_per_b};
+    const int dep = o.dep;
+    auto wait = [&]() {
+      if (dep >= 0) {
+        if (w0) {                                        // wave-uniform (scalar) poll loop
+          const unsigned need = (unsigned)ops[dep].items;
+          unsigned* c = done + dep * B + b;
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          for (unsigned spins = 0;; ++spins) {
+            const unsigned v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (v >= need) break;
+            __builtin_amdgcn_s_sleep(1);
+            // 20 ms (100 MHz clock) or 2^20 polls: give up, flag it
+            if (spins > (1u << 20) || __builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
+              __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+              break;
+            }
+          }
+        }
+        asm volatile("s_barrier" ::: "memory");          // orders the activation loads after the poll
+      }
+      if (ta.stamps) ts1 = __builtin_amdgcn_s_memrealtime();
+    };
+    switch (o.var) {
+#define SDDM_TEAM_CASE(S2V, MTV, NBV)                                                                  \
+  case team_var(S2V, MTV, NBV):                                                                        \
+    deep_tile<T, S2V, MTV, 4, 8, NBV, true>(o.a, te, tile, b, zb, smem, wait, ta.arena, hst);                         \
+    break;
+      SDDM_TEAM_CASE(false, 32, 16) SDDM_TEAM_CASE(false, 32, 32) SDDM_TEAM_CASE(false, 64, 16)
+      SDDM_TEAM_CASE(false, 64, 32) SDDM_TEAM_CASE(false, 128, 16) SDDM_TEAM_CASE(false, 128, 32)
+      SDDM_TEAM_CASE(true, 32, 16) SDDM_TEAM_CASE(true, 32, 32) SDDM_TEAM_CASE(true, 64, 16)
+      SDDM_TEAM_CASE(true, 64, 32)
+#undef SDDM_TEAM_CASE
+      default: break;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave: its stores reached the L2
+    __syncthreads();
+    if (w0) __hip_atomic_fetch_add(done + op * B + b, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ta.stamps && w0 && tk < 4096) {                  // (every lane of wave 0 stores the same words)
+      unsigned long long* st = ta.stamps + ((size_t)xcc * 4096 + tk) * 8;
+      st[0] = (unsigned long long)op | ((unsigned long long)b << 16);
+      st[1] = ts0; st[2] = ts1; st[3] = __builtin_amdgcn_s_memrealtime();
+    }
+  }
 }
 
 // weight-ring depth for a wave's K steps: the whole K when it fits in the register budget
@@ -468,6 +624,18 @@ int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps) {
   if (dtype == DT_F32) return 4;
   if (nw == 4 || mt >= 128) return 8;
   return deep_ring<bf16_t, 64, 8>(spw);
+}
+
+int conv_team_var(bool s2, int mt, int nb) {
+  if ((mt != 32 && mt != 64 && mt != 128) || (nb != 16 && nb != 32) || (s2 && mt == 128)) return -1;
+  return team_var(s2, mt, nb);
+}
+
+hipError_t launch_conv_team(int dtype, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s) {
+  if (dtype == DT_F32 || lds_bytes > kTeamLdsBudget || a.nops < 1 || blocks < 8) return hipErrorInvalidValue;
+  if (dtype == DT_BF16) hipLaunchKernelGGL(conv_team_kernel<bf16_t>, dim3(blocks), dim3(256), lds_bytes, s, a, a.ops);
+  else hipLaunchKernelGGL(conv_team_kernel<f16_t>, dim3(blocks), dim3(256), lds_bytes, s, a, a.ops);
+  return hipGetLastError();
 }
 
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a) {

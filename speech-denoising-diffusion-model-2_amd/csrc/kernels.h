@@ -42,6 +42,7 @@ struct ConvInArgs {
   float* stats;               // [B][tiles][Cout][2]
   int TR;                     // frame rows per block
   int* t_dev;                 // step counter decremented once per launch (may be null)
+  unsigned* zero; int nzero;  // words cleared by the launch (team-kernel counters of the step; may be null)
   unsigned long long* stamps; // SDDM_STAMPS builds only
 };
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s);
@@ -99,47 +100,30 @@ hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a);
 int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps);   // the D template argument (profiles)
 
-// ---- fused deep-level chain (conv_chain.hip, bf16 / f16) ----
-// One workgroup per image runs a sequence of convolution ops (the UNet levels whose images are
-// 32 or 128 pixels: Downsample -> ResnetBlocks -> mid -> ResnetBlocks -> Upsample, the reference's
-// UNetModified2.py:252-265 loop bodies at levels 4-5) with the activations and the GroupNorm
-// statistics resident in LDS; tensors that do not fit live in (L2-resident) global memory.
-struct ChainTensor {
-  int C, H, W;
-  int st;           // LDS byte offset of the per-channel (mean, M2) [C][2] fp32; -1: none
-  void* g;          // global [B][H][W][C] (T): the chain's input, its output, spilled / reloaded tensors
-  float* gst;       // global tile statistics [B][1][C][2] (sum, M2) for a GroupNorm consumer outside
+// ---- deep-level team kernel (conv_deep.hip): a run of consecutive convolutions as one launch,
+// image b served by the workgroups of XCD b % 8 through a ticket queue with per-(op, image)
+// completion counters (hand-offs stay in that XCD's L2) ----
+struct TeamOp {
+  ConvArgs a;                 // the layer's arguments exactly as its per-layer conv_deep launch
+  int var;                    // team_var(s2, mt, nb) (conv_deep.hip)
+  int items;                  // work items per image: n_tiles * Cout / nb
+  int toff;                   // column of the ResnetBlock's noise_func projection in the temb rows, -1: none
+  int dep;                    // op whose per-image completion this op waits for (-1: inputs precede the launch)
+  int pad[4];
 };
-struct ChainOp {
-  int kind;                    // 0 convolution, 1 reload (tensor a: global -> LDS image at a_lds)
-  int a, b, ra, rb, out;       // tensor indices: sources (virtual concat), residual sources, output
-  int s2, up, res_mode, gn, temb;
-  int var;                     // kernel variant (wave tiling), chosen on the host
-  int Cout;
-  const void* wf; const void* rwf;   // MFMA-fragment-major weights (ConvArgs::wgt_f / res_wgt_f)
-  const float* bias; const float* gamma; const float* beta;
-  int toff;                    // column of this ResnetBlock's noise_func projection in the temb rows
-  int HR, HC, PLB;             // staged halo rows / columns, plane stride of a staged 3x3 chunk
-  int stg, nslot, slot;        // staging buffer: LDS byte offset, chunks per group, bytes per chunk
-  int a_lds, b_lds, ra_lds, rb_lds;   // where this op reads each source: LDS image offset, -1 = global
-  int o_lds, o_gw;             // output: LDS image offset (-1: none), also stored to global
-};
-struct ChainArgs {
-  const ChainOp* ops; const ChainTensor* tens; int nops;   // device arrays (read through the constant cache)
+struct TeamArgs {
+  const TeamOp* ops; int nops; int B;
+  unsigned* ctr;              // [8 teams][32] ticket lines, then done [nops][B]; zeroed before every launch
+  unsigned* err;              // set to 1 when a dependency wait times out
   const float* temb; int temb_ld; const int* t_dev; int temb_per_b;
-  int groups; float eps;
-  int gsc, cmax;               // LDS: GN scale / shift [2][cmax]
-  int lds_bytes;
-  int dbg;                     // ablation bits (timing experiments, 0 in production): 1 no weight loads,
-                               // 2 no staging, 4 no MFMAs
-  unsigned long long* stamps;  // experiments: per image [32] s_memrealtime at op start / K loop end, [31] end
+  const char* arena;          // base of the lane arena holding every activation / statistics tensor (< 4 GiB)
+  unsigned long long* stamps; // experiments (SDDM_TEAM_STAMPS): per item [xcc * 4096 + ticket][8] =
+                              // {op | b << 16, s_memrealtime at ticket, after the wait, at publish,
+                              //  staged, K loop done, stored, statistics written}
 };
-// variant table (host): pixels per output image, 16-pixel fragments per wave, 16-channel
-// fragments per wave (a wave computes nfw or nfw - 1 of them)
-struct ChainVariant { int px, mfw, nfw; };
-int conv_chain_nvariants();
-ChainVariant conv_chain_variant(int v);
-hipError_t launch_conv_chain(int dtype, const ChainArgs& a, int B, hipStream_t s);
+constexpr int kTeamLdsBudget = 80 * 1024;    // two 4-wave workgroups per CU
+hipError_t launch_conv_team(int dtype, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s);
+int conv_team_var(bool s2, int mt, int nb);  // -1: no team variant for this tiling
 
 // ---- row-streaming 3x3 convolution for segment widths 64 / 128 (conv_strip.hip) ----
 hipError_t launch_conv_strip(int dtype, int nblk, int mpi, int SR, const ConvArgs& a, int B, hipStream_t s);

@@ -145,6 +145,10 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   const int b = blockIdx.y, f0 = blockIdx.x * a.TR, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   if (a.t_dev && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.t_dev -= 1;
+  // zero the step's team-kernel counters (ticket lines + completion counters, conv_deep.hip): the
+  // team launch later in this step finds them zero (kernel boundary in between)
+  if (a.zero && blockIdx.x == 0 && blockIdx.y == 0)
+    for (int i = tid; i < a.nzero; i += 256) a.zero[i] = 0u;
   SDDM_STAMP(a, 0);
   const int S = a.S, F = a.F, W = a.W, IW = W + 2, IH = a.TR + 2;
   {  // every load of the frame image issued before the first is stored (clamped addresses:

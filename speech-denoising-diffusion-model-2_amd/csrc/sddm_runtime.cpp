@@ -226,6 +226,7 @@ struct RunState {  // fields patched into the plan's kernel arguments at launch 
   int64_t row_offset = 0;
 };
 
+static constexpr int kTeamDefault = 0;  // deep-level team kernel off until it beats the per-layer launches
 static constexpr int kStreams = 4;    // concurrent lane streams (GPU_MAX_HW_QUEUES is 4)
 static constexpr int kMaxLanes = 64;  // step counters reserved in the weight arena
 
@@ -235,6 +236,7 @@ struct Lane {                         // one row block of the batch: plan + acti
   std::vector<Op> ops;
   RunState rs;
   size_t off_temb_fwd = 0, off_cond = 0, off_x = 0;
+  unsigned* team_err = nullptr;       // team kernel's wait-timeout word (zeroed at plan build)
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   int g_K = 0, g_gen = -1;
@@ -297,10 +299,11 @@ struct sddm_ctx {
   struct KernTune { int kind, a, b, c; };
   std::map<std::string, KernTune> kern_tune;
   int tune_B = -1, tune_dtype = -1, tune_N = -1;
-  // fused deep-level chain (conv_chain.hip): 1 = wherever the geometry allows, 0 = per-layer
-  // kernels only (tuning JSON key "chain"; SDDM_CHAIN overrides).  Off by default until it beats
-  // the per-layer kernels on the bench geometry.
-  int chain = 0;
+  // deep-level team kernel (conv_deep.hip conv_team_kernel): the consecutive 16-bit convolutions
+  // whose outputs have at most team_px pixels run as one launch per step (tuning JSON keys "team":
+  // 0 off, 1 on, 2 team tilings as per-layer launches, and "team_px"; SDDM_TEAM, SDDM_TEAM_PX override)
+  int team = kTeamDefault;
+  int team_px = 512;
   int hop_samples = 256;
 
   const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
@@ -498,6 +501,7 @@ struct ConvChoice {
   int nblk = 32, SR = 0, mpi = 128;
   int mt = 0, ckb = 0, nw = 4, nb = 32;           // conv_deep: pixels per block, input chunks, waves, channels
   int tile = -1;                                  // conv_tile configuration (16-bit dtypes), -1: none
+  int team = 0;                                   // conv_deep tiling chosen for the team kernel (nw = 4)
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
 };
 
@@ -553,6 +557,55 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
   ch.strip = 0; ch.mt = pick->mt; ch.nw = pick->nw; ch.nb = nb; ch.ckb = (a.CA + a.CB) / 32;
   ch.TR = pick->TR; ch.TW = pick->TW; ch.tiles_x = pick->tiles_x; ch.n_tiles = pick->n_tiles;
   return true;
+}
+
+// conv_deep tiling of a layer run by the team kernel (conv_team_kernel): 4 waves, 16 or 32 output
+// channels, LDS within two workgroups per CU.  A team is one XCD (64 workgroups) serving
+// ceil(PB / 8) images; per candidate the op's time is estimated as the larger of (rounds of
+// items x one item's latency: its L2 bytes at ~64 B/clk into one CU + its MFMA cycles + a fixed
+// ~1500 clk of hand-off and round trips) and the team's L2 bytes at ~2 KB/clk.  SDDM_TEAM_CFG=mt:nb
+// forces a tiling wherever it fits (experiments).
+static bool choose_team(int dt, int PB, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
+                        ConvChoice& ch) {
+  static int f_mt = -1, f_nb = 0;
+  if (f_mt < 0) {
+    f_mt = 0;
+    if (const char* e = std::getenv("SDDM_TEAM_CFG")) std::sscanf(e, "%d:%d", &f_mt, &f_nb);
+  }
+  if (dt == DT_F32 || Cin % 32 || RC % 32 || Cout % 16) return false;
+  ConvArgs a{};
+  a.CA = Cin; a.RCA = RC; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.upsample = up ? 1 : 0;
+  a.Hi = up ? Ho / 2 : (s2 ? Ho * 2 : Ho); a.Wi = up ? Wo / 2 : (s2 ? Wo * 2 : Wo);
+  a.deep_nw = 4;
+  const int nimg = (PB + 7) / 8, es = 2, K = 9 * Cin + (res_mode == 2 ? RC : 0);
+  double best = 1e30;
+  bool found = false;
+  for (int mt : {32, 64, 128})
+    for (int nb : {16, 32}) {
+      if (conv_team_var(s2, mt, nb) < 0 || Cout % nb) continue;
+      if (f_mt && (mt != f_mt || nb != f_nb)) continue;
+      const int TW = std::min(Wo, mt);
+      if (mt % TW || Wo % TW) continue;
+      const int TR = std::min(mt / TW, Ho);
+      if (Ho % TR || (TR * TW < mt && mt > 32)) continue;
+      a.TR = TR; a.TW = TW; a.tiles_x = Wo / TW; a.n_tiles = a.tiles_x * (Ho / TR); a.deep_nb = nb;
+      if (conv_deep_lds_bytes(dt, mt, s2, a) > (size_t)kTeamLdsBudget) continue;
+      const double halo = s2 ? (2.0 * TR + 1) * (2 * TW + 1) : (TR + 2.0) * (TW + 2);
+      const double item_bytes = (double)nb * K * es + halo * Cin * es + (res_mode == 2 ? (double)TR * TW * RC * es : 0) +
+                                (double)TR * TW * nb * es * (res_mode == 1 ? 2 : 1);
+      const double items = (double)a.n_tiles * (Cout / nb) * nimg;
+      const double mfma = (mt / 16.0) * (nb / 16.0) * (K / 32.0) * 8.0 / 4.0;
+      const double rounds = std::ceil(items / 64.0);
+      const double cost = std::max(rounds * (item_bytes / 64.0 + mfma + 1500.0), items * item_bytes / 2048.0);
+      if (cost < best) {
+        best = cost;
+        found = true;
+        ch = ConvChoice{};
+        ch.strip = 0; ch.mt = mt; ch.nw = 4; ch.nb = nb; ch.ckb = Cin / 32; ch.team = 1;
+        ch.TR = TR; ch.TW = TW; ch.tiles_x = a.tiles_x; ch.n_tiles = a.n_tiles;
+      }
+    }
+  return found;
 }
 
 // conv_tile configuration: the largest pixel x channel tile (most reuse of each transformed input
@@ -640,19 +693,6 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
   return choose_deep(dt, B, a, s2, ch, want_mt, want_nw, want_nb);
 }
 
-// staged halo of a conv_chain op (x: rows, y: padded row stride, z: plane stride in bytes): stride 1
-// (Ho + 2) x (Wo + 2); stride 2 as four polyphase planes of (Ho + 1) x (Wo + 1).  The row stride is
-// padded so a column-major 16-pixel MFMA fragment reads 16 distinct bank groups at every tap: odd
-// for 16-row outputs (one column per fragment), 2 mod 4 for 8-row ones (two columns)
-static dim3 chain_halo(int s2, int Ho, int Wo) {
-  const int HR = s2 ? Ho + 1 : Ho + 2;
-  int HC = s2 ? Wo + 1 : Wo + 2;
-  if (Ho >= 16 && HC % 2 == 0) HC += 1;
-  if (Ho == 8) while (HC % 4 != 2) ++HC;
-  const int units = (s2 ? 4 : 1) * HR * HC;
-  return dim3(HR, HC, (units * 16 + 255) / 256 * 256);
-}
-
 static int build_lane(sddm_ctx* c, Lane& L) {
   const int B = L.B;
   Lane* lp = &L;
@@ -686,7 +726,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   L.off_cond = A.reserve(sizeof(float) * (size_t)B * N);
   L.off_x = A.reserve(sizeof(float) * (size_t)B * N);
 
-  enum { ST_CONVIN, ST_GN, ST_CONV, ST_FINAL, ST_CHAIN };
+  enum { ST_CONVIN, ST_GN, ST_CONV, ST_FINAL, ST_TEAM };
   struct Step {
     int type = 0;
     std::string w;          // weight-name prefix
@@ -695,21 +735,17 @@ static int build_lane(sddm_ctx* c, Lane& L) {
     int s2 = 0, up = 0, res_mode = 0, rawA = -1, rawB = -1, cout = 0;
     bool temb = false;
     ConvChoice ch;
+    int team = -1;          // ST_TEAM: index into teams
   };
-  // fused deep-level chain: the conv steps it replaces, its tensor table (tres indices) and ops
-  // (conv ops in step order with reload ops between them; op_step[i] = step index or -1)
-  struct ChainPlan {
+  // deep-level team launches (conv_team_kernel): the conv steps each one runs, its op table
+  struct TeamPlan {
     std::vector<Step> steps;
-    std::vector<int> tens;                 // chain tensor -> tres index
-    std::vector<ChainTensor> ht;
-    std::vector<ChainOp> ho;
-    std::vector<int> op_step;
-    std::vector<int> gl;                   // chain tensor has a global copy the chain writes or reads
-    size_t off_ops = 0, off_tens = 0;
-    int lds_bytes = 0, gsc = 0, cmax = 0;
+    size_t off_ops = 0;
+    size_t ctr_word = 0;    // first counter word of this team in the step's counter block
   };
-  ChainPlan chain;
-  bool has_chain = false;
+  std::vector<TeamPlan> teams;
+  size_t off_err = 0, off_ctr = 0;
+  int n_ctr = 0;            // counter words conv_in clears every step
   std::vector<Step> prog;
   // measured per-layer deep tiles (sddm_set_conv_tuning) apply when they were measured for this
   // lane batch, dtype and length; otherwise the round-count heuristic of choose_deep decides
@@ -718,6 +754,15 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   // and GroupNorm tilings, hence bit-identical rows
   const int PB = std::max(1, c->lane_rows);
   const bool tuned = c->tune_B == PB && c->tune_dtype == dt && c->tune_N == N;
+  // the team kernel spreads a lane's images over the 8 XCDs: on by default for 16-bit lanes of 8+
+  // rows (SDDM_TEAM=1 forces it for any lane, SDDM_TEAM=0 turns it off)
+  static const char* env_team = std::getenv("SDDM_TEAM");
+  static const int env_team_px = std::getenv("SDDM_TEAM_PX") ? std::atoi(std::getenv("SDDM_TEAM_PX")) : 0;
+  // (mode 2: the team tilings, each layer still its own conv_deep launch: the bit-exact reference the
+  // tests compare the team launch with)
+  const int team_mode = env_team ? std::atoi(env_team) : c->team;
+  const bool team_on = dt != DT_F32 && team_mode != 0 && (env_team != nullptr || PB >= 8);
+  const int team_px = env_team_px > 0 ? env_team_px : c->team_px;
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
     int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;
@@ -730,6 +775,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         if (kind == 3) { wm = kt->second.a; wn = kt->second.b; wb = kt->second.c; }
       }
     }
+    if (team_on && Ho * Wo <= team_px && choose_team(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch)) return true;
     return choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka, wb);
   };
   const int TRin = 512 / W;
@@ -799,320 +845,35 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   const int gf = new_gn(cur, -1, "final_conv");
   { Step st; st.type = ST_FINAL; st.srcA = cur; st.gn = gf; prog.push_back(st); }
 
-  // ---- fused deep-level chain (conv_chain.hip): the contiguous run of conv steps whose output
-  // images have <= 128 pixels becomes one launch when every step fits a kernel variant and the
-  // LDS plan (activations + statistics + staging) fits ----
-  std::vector<int> chain_gst;   // chain tensor needs global tile statistics (GroupNorm consumer outside)
+  // ---- deep-level team launches: every run of >= 2 consecutive team-tiled conv steps becomes one
+  // conv_team_kernel launch (a lone one runs as its per-layer conv_deep launch, same tiling) ----
   {
-    static const char* env_chain = std::getenv("SDDM_CHAIN");
-    bool ok = (env_chain ? std::atoi(env_chain) != 0 : c->chain != 0) && dt != DT_F32 && es == 2;
-    int i0 = -1, i1 = -1;
-    for (int i = 0; ok && i < (int)prog.size(); ++i) {
-      const Step& st = prog[i];
-      if (st.type != ST_CONV || tres[st.out].H * tres[st.out].W > 128) continue;
-      if (i0 >= 0 && i != i1 + 1) ok = false;   // not one contiguous run
-      if (i0 < 0) i0 = i;
-      i1 = i;
-    }
-    if (i0 < 0) ok = false;
-    std::vector<int> producer(tres.size(), -1);
-    for (int i = 0; i < (int)prog.size(); ++i)
-      if (prog[i].out >= 0) producer[prog[i].out] = i;
-    auto inside = [&](int t) { return t >= 0 && producer[t] >= i0 && producer[t] <= i1; };
-    // what a step reads: (tensor, kind) with kind 0 staged 3x3 source, 1 GroupNorm statistics,
-    // 2 res_conv source (read as MFMA operands straight from LDS), 3 identity residual (epilogue)
-    auto reads = [&](const Step& st, std::vector<std::pair<int, int>>& r) {
-      r.clear();
-      for (int t : {st.srcA, st.srcB})
-        if (t >= 0) r.push_back({t, 0});
-      if (st.gn >= 0) {
-        if (gres[st.gn].a >= 0) r.push_back({gres[st.gn].a, 1});
-        if (gres[st.gn].b >= 0) r.push_back({gres[st.gn].b, 1});
-      }
-      if (st.res_mode == 2) {
-        for (int t : {st.rawA, st.rawB})
-          if (t >= 0) r.push_back({t, 2});
-      } else if (st.res_mode == 1 && st.rawA >= 0) {
-        r.push_back({st.rawA, 3});
-      }
-    };
-    std::vector<int> var(ok ? i1 - i0 + 1 : 0, -1);
-    for (int i = i0; ok && i <= i1; ++i) {
-      const Step& st = prog[i];
-      const int Cin = tres[st.srcA].C + (st.srcB >= 0 ? tres[st.srcB].C : 0);
-      const int RC = st.res_mode == 2 ? tres[st.rawA].C + (st.rawB >= 0 ? tres[st.rawB].C : 0) : 0;
-      const int Ho = tres[st.out].H, Wo = tres[st.out].W, P = Ho * Wo;
-      if (Cin % 32 || RC % 32 || st.cout % 16 || (st.srcB >= 0 && tres[st.srcB].C % 32) ||
-          (st.rawB >= 0 && tres[st.rawA].C % 32)) { ok = false; break; }
-      // a variant whose 4 waves each get NFW or NFW - 1 of the NF 16-channel fragments
-      const int NF = st.cout / 16;
-      for (int v = 0; v < conv_chain_nvariants() && var[i - i0] < 0; ++v) {
-        const ChainVariant cv = conv_chain_variant(v);
-        // (the kernel's fragment geometry: 128-pixel outputs are 16 x 8, 32-pixel ones 8 x 4)
-        if (cv.px == P && cv.mfw * 16 == P && Ho == (P == 128 ? 16 : 8) && 4 * (cv.nfw - 1) < NF && NF <= 4 * cv.nfw)
-          var[i - i0] = v;
-      }
-      if (var[i - i0] < 0) ok = false;
-    }
-    if (ok) {
-      ChainPlan& cp = chain;
-      std::map<int, int> cidx;   // tres -> chain tensor
-      std::vector<std::pair<int, int>> rd;
-      auto ci = [&](int t) -> int {
-        if (t < 0) return -1;
-        auto it = cidx.find(t);
-        if (it != cidx.end()) return it->second;
-        cidx[t] = (int)cp.tens.size();
-        cp.tens.push_back(t);
-        return (int)cp.tens.size() - 1;
-      };
-      for (int i = i0; i <= i1; ++i) {
-        reads(prog[i], rd);
-        for (auto& x : rd) ci(x.first);
-        ci(prog[i].out);
-      }
-      const int nt = (int)cp.tens.size(), nop = i1 - i0 + 1;
-      // uses in half-steps: op j reads its staged / res_conv sources and GroupNorm statistics at
-      // time 2j (K loop), its identity residual at 2j + 1 (epilogue), and writes its output at
-      // 2j + 1, so an output may take the LDS of inputs the op has finished with
-      struct Use { int time, kind; };
-      std::vector<std::vector<Use>> uses(nt);
-      std::vector<int> prod(nt, -1), used_out(nt, 0);
-      chain_gst.assign(nt, 0);
-      for (int k = 0; k < nt; ++k)
-        if (inside(cp.tens[k])) prod[k] = producer[cp.tens[k]] - i0;
-      for (int i = 0; i < (int)prog.size(); ++i) {
-        reads(prog[i], rd);
-        for (auto& x : rd) {
-          auto it = cidx.find(x.first);
-          if (it == cidx.end()) continue;
-          const int k = it->second;
-          if (i >= i0 && i <= i1) uses[k].push_back({2 * (i - i0) + (x.second == 3 ? 1 : 0), x.second});
-          else if (prod[k] >= 0) {
-            used_out[k] = 1;
-            if (x.second == 1) chain_gst[k] = 1;
-          }
-        }
-      }
-      for (int k = 0; k < nt; ++k) {
-        std::sort(uses[k].begin(), uses[k].end(), [](const Use& x, const Use& y) { return x.time < y.time; });
-        if (prod[k] < 0)   // chain inputs stay in global memory: staged 3x3 sources only
-          for (const Use& u : uses[k])
-            if (u.kind != 0) ok = false;
-      }
-      // LDS: [GN scale / shift 2 x cmax] then the planned items
-      int cmax = 0;
-      for (int i = i0; i <= i1; ++i) {
-        const Step& st = prog[i];
-        cmax = std::max({cmax, tres[st.srcA].C + (st.srcB >= 0 ? tres[st.srcB].C : 0), st.cout});
-      }
-      cp.cmax = cmax;
-      cp.gsc = 0;
-      // [GN scale / shift 2 x cmax][two parameter buffers 3 x cmax] fp32 (conv_chain.hip)
-      const int base = (32 * cmax + 255) / 256 * 256;
-      if (3 * cmax > 4 * 256) ok = false;
-      // residency: LDS segments per tensor (image uses in [t0, t1]); a segment after a gap in the
-      // uses starts with a reload from the tensor's global copy when a res_conv operand needs it,
-      // otherwise those uses read the global copy
-      struct Seg { int t0, t1; bool reload; int off; };
-      std::vector<std::vector<Seg>> segs(nt);
-      for (int k = 0; k < nt; ++k) {
-        int tl = -1;
-        for (const Use& u : uses[k])
-          if (u.kind != 1) tl = std::max(tl, u.time);
-        if (prod[k] >= 0 && tl >= 0) segs[k].push_back({2 * prod[k] + 1, tl, false, -1});
-      }
-      auto seg_uses = [&](int k, const Seg& sg) {
-        std::vector<Use> r;
-        for (const Use& u : uses[k])
-          if (u.kind != 1 && u.time >= sg.t0 && u.time <= sg.t1) r.push_back(u);
-        return r;
-      };
-      // park tensor k over the largest gap between two of its image uses (false: none to split)
-      auto park = [&](int k) -> bool {
-        int best_s = -1, best_gap = 0, best_at = 0;
-        for (size_t si = 0; si < segs[k].size(); ++si) {
-          const std::vector<Use> su = seg_uses(k, segs[k][si]);
-          int prev = segs[k][si].t0;
-          for (const Use& u : su) {
-            if (u.time - prev > best_gap) { best_gap = u.time - prev; best_s = (int)si; best_at = prev; }
-            prev = u.time;
-          }
-        }
-        if (best_s < 0 || best_gap < 3) return false;
-        Seg a0 = segs[k][best_s];
-        std::vector<Use> later;
-        for (const Use& u : seg_uses(k, a0))
-          if (u.time > best_at) later.push_back(u);
-        segs[k].erase(segs[k].begin() + best_s);
-        if (best_at > a0.t0) segs[k].push_back({a0.t0, best_at, a0.reload, -1});
-        int first_res = -1;
-        for (const Use& u : later)
-          if (u.kind == 2) { first_res = u.time; break; }
-        if (first_res >= 0) {   // reload before the first use after the gap that needs LDS
-          int t0 = later.front().time;
-          t0 = t0 - (t0 & 1);    // the K phase of that op
-          segs[k].push_back({t0, later.back().time, true, -1});
-        }
-        std::sort(segs[k].begin(), segs[k].end(), [](const Seg& x, const Seg& y) { return x.t0 < y.t0; });
-        return true;
-      };
-      std::vector<int> stg_off(nop, 0), nslot(nop, 0), slot(nop, 0), st_off(nt, -1);
-      int total = 0;
-      for (int attempt = 0; ok; ++attempt) {
-        struct Item { int s, e, size, al, k, si, off; };
-        std::vector<Item> items;
-        for (int k = 0; k < nt; ++k) {
-          const TRes& r = tres[cp.tens[k]];
-          for (size_t si = 0; si < segs[k].size(); ++si)
-            items.push_back({segs[k][si].t0, segs[k][si].t1, r.C * r.H * r.W * 2, 256, k, (int)si, -1});
-          int sl = -1;
-          for (const Use& u : uses[k])
-            if (u.kind == 1) sl = std::max(sl, u.time);
-          if (sl >= 0 && prod[k] >= 0) items.push_back({2 * prod[k] + 1, sl, r.C * 8, 16, k, -1, -1});
-        }
-        std::stable_sort(items.begin(), items.end(), [](const Item& x, const Item& y) {
-          return x.s != y.s ? x.s < y.s : x.size > y.size;
-        });
-        for (size_t n = 0; n < items.size(); ++n) {   // first fit over lifetimes
-          Item& it = items[n];
-          int off = 0;
-          for (bool moved = true; moved;) {
-            moved = false;
-            for (size_t m = 0; m < n; ++m) {
-              const Item& o = items[m];
-              if (o.e < it.s || o.s > it.e) continue;   // lifetimes disjoint
-              if (off + it.size <= o.off || off >= o.off + o.size) continue;
-              off = (o.off + o.size + it.al - 1) / it.al * it.al;
-              moved = true;
-            }
-          }
-          it.off = off;
-        }
-        // each op's staging buffer sits above everything live during its K loop and takes the room
-        // left: as many 32-channel chunk slots as fit
-        bool fits = true;
-        total = base;
-        for (const Item& it : items) total = std::max(total, base + it.off + it.size);
-        for (int j = 0; j < nop && fits; ++j) {
-          const Step& st = prog[i0 + j];
-          int top = 0;
-          for (const Item& it : items)
-            if (it.s <= 2 * j && 2 * j <= it.e) top = std::max(top, it.off + it.size);
-          const int PLB = chain_halo(st.s2, tres[st.out].H, tres[st.out].W).z;
-          const int nck = (tres[st.srcA].C + (st.srcB >= 0 ? tres[st.srcB].C : 0)) / 32;
-          const int off = (top + 255) / 256 * 256;
-          const int ns = std::min(nck, (160 * 1024 - base - off) / (4 * PLB));
-          if (ns < 1) { fits = false; break; }
-          stg_off[j] = base + off; nslot[j] = ns; slot[j] = 4 * PLB;
-          total = std::max(total, base + off + ns * 4 * PLB);
-        }
-        if (fits && total <= 160 * 1024) {
-          for (const Item& it : items) {
-            if (it.si >= 0) segs[it.k][it.si].off = base + it.off;
-            else st_off[it.k] = base + it.off;
-          }
-          break;
-        }
-        // over budget: park the biggest tensor x gap that can be parked
-        int pick = -1;
-        long best = -1;
-        for (int k = 0; k < nt; ++k) {
-          if (segs[k].empty()) continue;
-          const TRes& r = tres[cp.tens[k]];
-          int span = 0;
-          for (const Seg& sg : segs[k]) span += sg.t1 - sg.t0;
-          const long score = (long)span * r.C * r.H * r.W;
-          if (score > best) {
-            std::vector<std::vector<Seg>> save = segs;
-            if (park(k)) { segs = save; best = score; pick = k; }
-            else segs = save;
-          }
-        }
-        if (pick < 0 || attempt > 64) { ok = false; break; }
-        park(pick);
-      }
-      if (ok) {
-        cp.lds_bytes = total;
-        auto lds_at = [&](int k, int t) -> int {
-          if (k < 0) return -1;
-          for (const Seg& sg : segs[k])
-            if (sg.t0 <= t && t <= sg.t1) return sg.off;
-          return -1;
-        };
-        cp.gl.assign(nt, 0);
-        for (int k = 0; k < nt; ++k) {
-          cp.gl[k] = prod[k] < 0 || used_out[k];
-          for (const Seg& sg : segs[k]) cp.gl[k] |= sg.reload;
-          for (const Use& u : uses[k])
-            if (u.kind != 1 && lds_at(k, u.time) < 0) cp.gl[k] = 1;
-          if (prod[k] >= 0 && segs[k].empty() && uses[k].empty()) cp.gl[k] = 1;
-        }
-        cp.ht.assign(nt, ChainTensor{});
-        for (int k = 0; k < nt; ++k) {
-          TRes& r = tres[cp.tens[k]];
-          ChainTensor& t = cp.ht[k];
-          t.C = r.C; t.H = r.H; t.W = r.W;
-          t.st = st_off[k];
-          if (chain_gst[k]) { r.tiles = 1; r.n_tile = r.H * r.W; }   // per-image statistics for the consumer
-        }
-        for (int j = 0; j < nop; ++j) {
-          const Step& st = prog[i0 + j];
-          for (int k = 0; k < nt; ++k)   // reloads before this op
-            for (const Seg& sg : segs[k])
-              if (sg.reload && sg.t0 == 2 * j) {
-                ChainOp r{};
-                r.kind = 1; r.a = k; r.a_lds = sg.off; r.b = r.ra = r.rb = r.out = -1;
-                cp.ho.push_back(r);
-                cp.op_step.push_back(-1);
-              }
-          ChainOp o{};
-          o.kind = 0;
-          o.a = ci(st.srcA); o.b = ci(st.srcB); o.out = ci(st.out);
-          o.ra = st.res_mode ? ci(st.rawA) : -1; o.rb = st.res_mode == 2 ? ci(st.rawB) : -1;
-          o.s2 = st.s2; o.up = st.up; o.res_mode = st.res_mode; o.gn = st.gn >= 0; o.temb = st.temb;
-          o.var = var[j]; o.Cout = st.cout;
-          const dim3 hg = chain_halo(st.s2, tres[st.out].H, tres[st.out].W);
-          o.HR = hg.x; o.HC = hg.y; o.PLB = hg.z;
-          o.stg = stg_off[j]; o.nslot = nslot[j]; o.slot = slot[j];
-          o.a_lds = lds_at(o.a, 2 * j); o.b_lds = lds_at(o.b, 2 * j);
-          o.ra_lds = lds_at(o.ra, st.res_mode == 1 ? 2 * j + 1 : 2 * j); o.rb_lds = lds_at(o.rb, 2 * j);
-          o.o_lds = lds_at(o.out, 2 * j + 1); o.o_gw = cp.gl[o.out];
-          if (st.res_mode == 2 && (o.ra_lds < 0 || (o.rb >= 0 && o.rb_lds < 0))) ok = false;   // res_conv operands from LDS
-          cp.ho.push_back(o);
-          cp.op_step.push_back(j);
-          cp.steps.push_back(st);
-        }
-      }
-      if (ok && std::getenv("SDDM_CHAIN_DEBUG")) {   // the LDS plan (experiments)
-        fprintf(stderr, "chain %s..%s: %d ops, LDS %d bytes (cmax %d)\n", prog[i0].w.c_str(), prog[i1].w.c_str(),
-                (int)cp.ho.size(), cp.lds_bytes, cp.cmax);
-        for (int k = 0; k < nt; ++k) {
-          fprintf(stderr, "  tensor %d: C %d %dx%d st %d global %d gst %d segments", k, cp.ht[k].C, cp.ht[k].H,
-                  cp.ht[k].W, cp.ht[k].st, cp.gl[k], chain_gst[k]);
-          for (const Seg& sg : segs[k]) fprintf(stderr, " [%d,%d]%s@%d", sg.t0, sg.t1, sg.reload ? "r" : "", sg.off);
-          fprintf(stderr, "\n");
-        }
-        for (size_t i = 0; i < cp.ho.size(); ++i) {
-          const ChainOp& o = cp.ho[i];
-          if (o.kind == 1) { fprintf(stderr, "  op %zu reload tensor %d -> %d\n", i, o.a, o.a_lds); continue; }
-          fprintf(stderr, "  op %zu %s: var %d a %d(%d) b %d(%d) ra %d(%d) rb %d(%d) out %d(%d, gw %d) stg %d x %d slots of %d\n",
-                  i, cp.steps[cp.op_step[i]].w.c_str(), o.var, o.a, o.a_lds, o.b, o.b_lds, o.ra, o.ra_lds, o.rb, o.rb_lds,
-                  o.out, o.o_lds, o.o_gw, o.stg, o.nslot, o.slot);
-        }
-      }
-      if (ok) {
-        cp.off_ops = A.reserve(sizeof(ChainOp) * cp.ho.size());
-        cp.off_tens = A.reserve(sizeof(ChainTensor) * cp.ht.size());
-        Step cs;
-        cs.type = ST_CHAIN;
-        prog.erase(prog.begin() + i0, prog.begin() + i1 + 1);
-        prog.insert(prog.begin() + i0, cs);
-        has_chain = true;
+    std::vector<Step> np;
+    for (size_t i = 0; i < prog.size();) {
+      size_t j = i;
+      while (j < prog.size() && prog[j].type == ST_CONV && prog[j].ch.team) ++j;
+      if (j - i >= 2 && team_mode != 2 && A.used < ((size_t)1 << 32)) {   // hand-off loads address the arena with 32-bit offsets
+        TeamPlan tp;
+        tp.steps.assign(prog.begin() + i, prog.begin() + j);
+        tp.off_ops = A.reserve(sizeof(TeamOp) * tp.steps.size());
+        tp.ctr_word = (size_t)n_ctr;
+        n_ctr += 8 * 32 + (int)tp.steps.size() * B;
+        Step ts;
+        ts.type = ST_TEAM;
+        ts.team = (int)teams.size();
+        teams.push_back(tp);
+        np.push_back(ts);
+        i = j;
+      } else if (j > i) {
+        for (; i < j; ++i) np.push_back(prog[i]);
       } else {
-        cp = ChainPlan{};
-        chain_gst.clear();
+        np.push_back(prog[i++]);
       }
+    }
+    prog.swap(np);
+    if (!teams.empty()) {
+      off_err = A.reserve(256);
+      off_ctr = A.reserve(sizeof(unsigned) * (size_t)n_ctr);
     }
   }
   SDDM_HIP_CHECK(A.commit());
@@ -1128,6 +889,50 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   };
   auto WF = [&](const std::string& k) { return c->warena.at<float>(c->woff.at(k)); };
   auto WV = [&](const std::string& k) { return (const void*)(c->warena.base + c->woff.at(k)); };
+  // the kernel arguments of one conv step (per-layer launch or team op), its algorithmic bytes and FLOPs
+  auto conv_args = [&](const Step& st, ConvArgs& a, double& bytes, double& flops) -> int {
+    a = ConvArgs{};
+    const Tensor sa = TT(st.srcA), sb = TT(st.srcB), o = TT(st.out);
+    a.srcA = sa.p; a.srcB = sb.p; a.CA = sa.C; a.CB = sb.C;
+    a.Hi = sa.H; a.Wi = sa.W; a.Ho = o.H; a.Wo = o.W; a.upsample = st.up;
+    a.Cout = st.cout; a.out = o.p; a.stats = o.stats;
+    if (st.gn >= 0) {
+      const GNRes& gr = gres[st.gn];
+      const Tensor ga = TT(gr.a), gb = TT(gr.b);
+      a.gstA = ga.stats; a.gtilesA = ga.tiles; a.gntileA = ga.n_tile;
+      a.gstB = gb.stats; a.gtilesB = gb.tiles; a.gntileB = gb.n_tile;
+      a.gamma = WF(gr.w + ".gamma"); a.beta = WF(gr.w + ".beta"); a.groups = u.groups; a.eps = 1e-5f;
+      const int Ct = ga.C + gb.C;
+      if (Ct % u.groups || (gb.C && ga.C % (Ct / u.groups)) || 256 % u.groups)
+        FAIL(SDDM_ERR_SHAPE, "GroupNorm(%d, %d) at %s: unsupported grouping", u.groups, Ct, gr.w.c_str());
+    }
+    a.wgt = WV(st.w + ".w"); a.bias = WF(st.w + ".b");
+    a.wgt_t = c->woff.count(st.w + ".w_t") ? WV(st.w + ".w_t") : nullptr;
+    a.wgt_f = WV(st.w + ".w_f");
+    a.res_mode = st.res_mode;
+    const int Cin = a.CA + a.CB;
+    bytes = (double)B * a.Hi * a.Wi * Cin * es + (double)B * a.Ho * a.Wo * a.Cout * es +
+            (double)a.Cout * 9 * Cin * es;
+    flops = 2.0 * B * a.Ho * a.Wo * a.Cout * 9.0 * Cin;
+    if (st.res_mode == 1) {
+      a.res_src = TT(st.rawA).p;
+      bytes += (double)B * a.Ho * a.Wo * a.Cout * es;
+    } else if (st.res_mode == 2) {
+      const Tensor ra = TT(st.rawA), rb = TT(st.rawB);
+      a.rawA = ra.p; a.rawB = rb.p; a.RCA = ra.C; a.RCB = rb.C;
+      a.res_wgt = WV(st.rb + ".res.w");
+      a.res_wgt_t = c->woff.count(st.rb + ".res.w_t") ? WV(st.rb + ".res.w_t") : nullptr;
+      a.res_wgt_f = WV(st.rb + ".res.w_f");
+      if ((ra.C + rb.C) % 32) FAIL(SDDM_ERR_SHAPE, "%s.res_conv: channels must be multiples of 32", st.rb.c_str());
+      bytes += (double)B * a.Ho * a.Wo * (ra.C + rb.C) * es + (double)a.Cout * (ra.C + rb.C) * es;
+      flops += 2.0 * B * a.Ho * a.Wo * a.Cout * (double)(ra.C + rb.C);
+    }
+    const ConvChoice& ch = st.ch;
+    a.TR = ch.TR; a.TW = ch.TW; a.tiles_x = ch.tiles_x; a.n_tiles = ch.n_tiles;
+    if (a.n_tiles != o.tiles || a.TR * a.TW != o.n_tile) FAIL(SDDM_ERR_STATE, "tile mismatch for %s", st.w.c_str());
+    if ((a.CA + a.CB) % 32 || a.Cout % 32) FAIL(SDDM_ERR_SHAPE, "%s: channels must be multiples of 32", st.w.c_str());
+    return SDDM_OK;
+  };
   sddm_ctx* ctx = c;
   for (const Step& st : prog) {
     if (st.type == ST_CONVIN) {
@@ -1136,6 +941,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       a.w = WF("downs.0.weight"); a.bias = WF("downs.0.bias");
       const Tensor o = TT(st.out);
       a.out = o.p; a.stats = o.stats; a.TR = TRin;
+      if (n_ctr) { a.zero = A.at<unsigned>(off_ctr); a.nzero = n_ctr; }
       const double bytes = (double)B * N * 4 * 2 + (double)B * F * W * u.inner * es;
       const double flops = 2.0 * B * F * W * u.inner * 18;
 #ifdef SDDM_STAMPS
@@ -1154,47 +960,12 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       L.ops.back().kname = std::string("conv_in_kernel<") + dt_name(dt) + ">";
       L.ops.back().kinst = L.ops.back().kname;
     } else if (st.type == ST_CONV) {
-      ConvArgs a{};
-      const Tensor sa = TT(st.srcA), sb = TT(st.srcB), o = TT(st.out);
-      a.srcA = sa.p; a.srcB = sb.p; a.CA = sa.C; a.CB = sb.C;
-      a.Hi = sa.H; a.Wi = sa.W; a.Ho = o.H; a.Wo = o.W; a.upsample = st.up;
-      a.Cout = st.cout; a.out = o.p; a.stats = o.stats;
-      if (st.gn >= 0) {
-        const GNRes& gr = gres[st.gn];
-        const Tensor ga = TT(gr.a), gb = TT(gr.b);
-        a.gstA = ga.stats; a.gtilesA = ga.tiles; a.gntileA = ga.n_tile;
-        a.gstB = gb.stats; a.gtilesB = gb.tiles; a.gntileB = gb.n_tile;
-        a.gamma = WF(gr.w + ".gamma"); a.beta = WF(gr.w + ".beta"); a.groups = u.groups; a.eps = 1e-5f;
-        const int Ct = ga.C + gb.C;
-        if (Ct % u.groups || (gb.C && ga.C % (Ct / u.groups)) || 256 % u.groups)
-          FAIL(SDDM_ERR_SHAPE, "GroupNorm(%d, %d) at %s: unsupported grouping", u.groups, Ct, gr.w.c_str());
-      }
-      a.wgt = WV(st.w + ".w"); a.bias = WF(st.w + ".b");
-      a.wgt_t = c->woff.count(st.w + ".w_t") ? WV(st.w + ".w_t") : nullptr;
-      a.wgt_f = WV(st.w + ".w_f");
-      a.res_mode = st.res_mode;
+      ConvArgs a;
+      double bytes = 0, flops = 0;
+      if (const int r = conv_args(st, a, bytes, flops)) return r;
       const int Cin = a.CA + a.CB;
-      double bytes = (double)B * a.Hi * a.Wi * Cin * es + (double)B * a.Ho * a.Wo * a.Cout * es +
-                     (double)a.Cout * 9 * Cin * es;
-      double flops = 2.0 * B * a.Ho * a.Wo * a.Cout * 9.0 * Cin;
-      if (st.res_mode == 1) {
-        a.res_src = TT(st.rawA).p;
-        bytes += (double)B * a.Ho * a.Wo * a.Cout * es;
-      } else if (st.res_mode == 2) {
-        const Tensor ra = TT(st.rawA), rb = TT(st.rawB);
-        a.rawA = ra.p; a.rawB = rb.p; a.RCA = ra.C; a.RCB = rb.C;
-        a.res_wgt = WV(st.rb + ".res.w");
-        a.res_wgt_t = c->woff.count(st.rb + ".res.w_t") ? WV(st.rb + ".res.w_t") : nullptr;
-        a.res_wgt_f = WV(st.rb + ".res.w_f");
-        if ((ra.C + rb.C) % 32) FAIL(SDDM_ERR_SHAPE, "%s.res_conv: channels must be multiples of 32", st.rb.c_str());
-        bytes += (double)B * a.Ho * a.Wo * (ra.C + rb.C) * es + (double)a.Cout * (ra.C + rb.C) * es;
-        flops += 2.0 * B * a.Ho * a.Wo * a.Cout * (double)(ra.C + rb.C);
-      }
       const ConvChoice ch = st.ch;
       const bool s2 = st.s2 != 0;
-      a.TR = ch.TR; a.TW = ch.TW; a.tiles_x = ch.tiles_x; a.n_tiles = ch.n_tiles;
-      if (a.n_tiles != o.tiles || a.TR * a.TW != o.n_tile) FAIL(SDDM_ERR_STATE, "tile mismatch for %s", st.w.c_str());
-      if (Cin % 32 || a.Cout % 32) FAIL(SDDM_ERR_SHAPE, "%s: channels must be multiples of 32", st.w.c_str());
       const bool temb = st.temb;
       const int toff = temb ? c->temb_off.at(st.rb) : 0;
 #ifdef SDDM_STAMPS
@@ -1266,80 +1037,56 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         };
         (void)base;
       }
-    } else if (st.type == ST_CHAIN) {
-      ChainPlan& cp = chain;
+    } else if (st.type == ST_TEAM) {
+      TeamPlan& tp = teams[st.team];
+      std::vector<TeamOp> ops(tp.steps.size());
       double bytes = 0, flops = 0;
-      for (size_t k = 0; k < cp.tens.size(); ++k) {
-        const Tensor t = TT(cp.tens[k]);
-        cp.ht[k].g = t.p;
-        cp.ht[k].gst = chain_gst[k] ? t.stats : nullptr;
+      int lds = 0;
+      for (size_t i = 0; i < tp.steps.size(); ++i) {
+        const Step& ms = tp.steps[i];
+        TeamOp& o = ops[i];
+        o = TeamOp{};
+        double by = 0, fl = 0;
+        if (const int r = conv_args(ms, o.a, by, fl)) return r;
+        bytes += by; flops += fl;
+        o.a.deep_nw = 4; o.a.deep_nb = ms.ch.nb; o.a.ck_batch = ms.ch.ckb;
+        o.var = conv_team_var(ms.s2 != 0, ms.ch.mt, ms.ch.nb);
+        if (o.var < 0) FAIL(SDDM_ERR_STATE, "no team variant for %s", ms.w.c_str());
+        o.items = o.a.n_tiles * (o.a.Cout / ms.ch.nb);
+        o.toff = ms.temb ? c->temb_off.at(ms.rb) : -1;
+        o.dep = (int)i - 1;            // every op reads its predecessor's output
+        static const int team_dbg = std::getenv("SDDM_TEAM_DBG") ? std::atoi(std::getenv("SDDM_TEAM_DBG")) : 0;
+        o.a.dbg = team_dbg;            // ablation bits of conv_deep (timing experiments only)
+        lds = std::max(lds, (int)conv_deep_lds_bytes(dt, ms.ch.mt, ms.s2 != 0, o.a));
+        if (std::getenv("SDDM_PLAN_DEBUG"))
+          fprintf(stderr, "team op %zu %s: mt %d nb %d tiles %d items/img %d Cin %d Cout %d gn tiles %d+%d lds %zu\n", i,
+                  ms.w.c_str(), ms.ch.mt, ms.ch.nb, o.a.n_tiles, o.items, o.a.CA + o.a.CB, o.a.Cout, o.a.gtilesA,
+                  o.a.gtilesB, conv_deep_lds_bytes(dt, ms.ch.mt, ms.s2 != 0, o.a));
       }
-      std::set<int> produced;
-      for (const Step& s : cp.steps) produced.insert(s.out);
-      for (size_t k = 0; k < cp.tens.size(); ++k) {   // algorithmic bytes: the chain's inputs read once,
-        const ChainTensor& t = cp.ht[k];             // its outputs consumed outside written once
-        const double sz = (double)B * t.C * t.H * t.W * es;
-        if (!produced.count(cp.tens[k])) bytes += sz;
-        else if (chain_gst[k] || cp.gl[k]) {
-          bool outside = false;
-          for (const Step& s2 : prog)
-            if (s2.type != ST_CHAIN)
-              for (int x : {s2.srcA, s2.srcB, s2.rawA, s2.rawB})
-                if (x == cp.tens[k]) outside = true;
-          if (outside) bytes += sz;
-        }
-      }
-      for (size_t i = 0; i < cp.ho.size(); ++i) {
-        if (cp.op_step[i] < 0) continue;   // reload
-        const Step& s = cp.steps[cp.op_step[i]];
-        ChainOp& o = cp.ho[i];
-        o.wf = WV(s.w + ".w_f");
-        o.rwf = s.res_mode == 2 ? WV(s.rb + ".res.w_f") : o.wf;
-        o.bias = WF(s.w + ".b");
-        o.gamma = s.gn >= 0 ? WF(gres[s.gn].w + ".gamma") : nullptr;
-        o.beta = s.gn >= 0 ? WF(gres[s.gn].w + ".beta") : nullptr;
-        o.toff = s.temb ? c->temb_off.at(s.rb) : 0;
-        const ChainTensor& ta = cp.ht[o.a];
-        const int Cin = ta.C + (o.b >= 0 ? cp.ht[o.b].C : 0);
-        const int RC = s.res_mode == 2 ? cp.ht[o.ra].C + (o.rb >= 0 ? cp.ht[o.rb].C : 0) : 0;
-        const ChainTensor& to = cp.ht[o.out];
-        const double P = (double)to.H * to.W;
-        flops += 2.0 * B * P * s.cout * (9.0 * Cin + RC);
-        bytes += ((double)s.cout * 9 * Cin + (double)s.cout * RC) * es;
-        if (s.gn >= 0) {
-          const Tensor ga = TT(gres[s.gn].a), gb = TT(gres[s.gn].b);
-          const int Ct = ga.C + gb.C;
-          if (Ct % u.groups || (gb.C && ga.C % (Ct / u.groups)) || 256 % u.groups)
-            FAIL(SDDM_ERR_SHAPE, "GroupNorm(%d, %d) at %s: unsupported grouping", u.groups, Ct, gres[s.gn].w.c_str());
-        }
-      }
-      SDDM_HIP_CHECK(hipMemcpy(A.base + cp.off_ops, cp.ho.data(), sizeof(ChainOp) * cp.ho.size(), hipMemcpyHostToDevice));
-      SDDM_HIP_CHECK(hipMemcpy(A.base + cp.off_tens, cp.ht.data(), sizeof(ChainTensor) * cp.ht.size(), hipMemcpyHostToDevice));
-      ChainArgs a{};
-      a.ops = A.at<ChainOp>(cp.off_ops);
-      a.tens = A.at<ChainTensor>(cp.off_tens);
-      a.nops = (int)cp.ho.size();
-      a.groups = u.groups; a.eps = 1e-5f;
-      a.gsc = cp.gsc; a.cmax = cp.cmax; a.lds_bytes = cp.lds_bytes;
-      static const int chain_dbg = std::getenv("SDDM_CHAIN_ABL") ? std::atoi(std::getenv("SDDM_CHAIN_ABL")) : 0;
-      a.dbg = chain_dbg;
-      if (std::getenv("SDDM_CHAIN_STAMPS")) {   // per-op timestamps (experiments; sddm_debug_stamps)
+      if (lds > kTeamLdsBudget) FAIL(SDDM_ERR_STATE, "team LDS %d bytes", lds);
+      SDDM_HIP_CHECK(hipMemcpy(A.base + tp.off_ops, ops.data(), sizeof(TeamOp) * ops.size(), hipMemcpyHostToDevice));
+      SDDM_HIP_CHECK(hipMemset(A.base + off_err, 0, 256));
+      TeamArgs ta{};
+      ta.ops = A.at<TeamOp>(tp.off_ops); ta.nops = (int)ops.size(); ta.B = B;
+      ta.ctr = A.at<unsigned>(off_ctr) + tp.ctr_word; ta.err = A.at<unsigned>(off_err);
+      ta.arena = (const char*)A.base;
+      if (std::getenv("SDDM_TEAM_STAMPS")) {   // per-item timestamps (experiments; sddm_debug_stamps)
         if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
         SDDM_HIP_CHECK(hipMemset(c->stamp_buf, 0, sizeof(unsigned long long) * 8 * 65536));
-        a.stamps = c->stamp_buf;
-        c->stamp_blocks = (int64_t)B * 8;
+        ta.stamps = c->stamp_buf;
+        c->stamp_blocks = 8 * 4096;          // [8 teams][4096 tickets][8 words]
       }
-      const std::string nm = "chain[" + cp.steps.front().w + ".." + cp.steps.back().w + "]";
-      L.ops.push_back({2, bytes, flops, [ctx, lp, a, dt, B](hipStream_t s) {
-                          ChainArgs x = a;
-                          x.temb = lp->rs.temb;
-                          x.temb_ld = ctx->SC;
+      const int blocks = 8 * 64;       // two 4-wave workgroups on each of an XCD's 32 CUs
+      const std::string nm = "team[" + tp.steps.front().w + ".." + tp.steps.back().w + "]";
+      L.ops.push_back({2, bytes, flops, [ctx, lp, ta, lds, blocks, dt](hipStream_t s) {
+                          TeamArgs x = ta;
+                          x.temb = lp->rs.temb; x.temb_ld = ctx->SC; x.t_dev = lp->rs.t_dev;
                           x.temb_per_b = lp->rs.temb_per_b;
-                          x.t_dev = lp->rs.t_dev;
-                          return launch_conv_chain(dt, x, B, s);
+                          return launch_conv_team(dt, x, lds, blocks, s);
                         }, nm});
-      L.ops.back().kname = std::string("conv_chain_kernel<") + dt_name(dt) + ">";
+      L.ops.back().kname = std::string("conv_team_kernel<") + dt_name(dt) + ">";
       L.ops.back().kinst = L.ops.back().kname;
+      L.team_err = ta.err;
     } else {
       FinalArgs f{};
       const Tensor src = TT(st.srcA);
@@ -1434,6 +1181,21 @@ static int prof_drain(sddm_ctx* c, const Lane& L) {
     a.ms += m; a.n += 1; a.bytes += L.ops[pe.first].bytes; a.flops += L.ops[pe.first].flops;
   }
   c->ev_pend.clear();
+  return SDDM_OK;
+}
+
+// SDDM_TEAM_CHECK=1 (tests): after a call, wait for it and fail if a team kernel's dependency wait
+// timed out (its results would be wrong; the kernel never hangs)
+static int team_check(sddm_ctx* c, hipStream_t s) {
+  const char* e = std::getenv("SDDM_TEAM_CHECK");
+  if (!e || std::atoi(e) == 0) return SDDM_OK;
+  SDDM_HIP_CHECK(hipStreamSynchronize(s));
+  for (auto& Lp : c->lanes)
+    if (Lp->team_err) {
+      unsigned e = 0;
+      SDDM_HIP_CHECK(hipMemcpy(&e, Lp->team_err, sizeof(e), hipMemcpyDeviceToHost));
+      if (e) FAIL(SDDM_ERR_HIP, "team kernel dependency wait timed out (lane %d)", Lp->idx);
+    }
   return SDDM_OK;
 }
 
@@ -1846,7 +1608,7 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
       SDDM_HIP_CHECK(hipEventRecord(c->ev_done[k], c->work[k]));
       SDDM_HIP_CHECK(hipStreamWaitEvent(user, c->ev_done[k], 0));
     }
-    return SDDM_OK;
+    return team_check(c, user);
   }
   int64_t nrec = 0;
   for (int t = T; t >= 1; --t) {
@@ -1859,7 +1621,7 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
       ++nrec;
     }
   }
-  return SDDM_OK;
+  return team_check(c, user);
 }
 
 int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const float* noise_level, int64_t B,
@@ -1889,7 +1651,7 @@ int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const
     r = run_ops(c, L, s);
     if (r) return r;
   }
-  return SDDM_OK;
+  return team_check(c, s);
 }
 
 int sddm_transition(sddm_ctx* c, int mode, const float* x_t, const float* eps, const float* cond, int t, int64_t B,
@@ -1977,7 +1739,8 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
       if (t.kind == 2 && (t.a < 0 || t.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), t.a);
       c->kern_tune[kv.first] = t;
     }
-  c->chain = (int)j.number("chain", 0) != 0 ? 1 : 0;
+  c->team = (int)j.number("team", kTeamDefault);
+  c->team_px = (int)j.number("team_px", 512);
   c->tune_B = (int)j.number("lane_batch", -1);
   c->tune_dtype = dt;
   c->tune_N = (int)j.number("num_samples", -1);

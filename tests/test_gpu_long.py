@@ -8,9 +8,15 @@ made by tests/golden/gen_golden.py --only long from /root/reference with the Phi
   * WaveGrad + SDDM_spectrogram.infer, T=50 (SURVEY §8d fast schedule; 54 frames, B=2: the reference
     WaveGrad cannot run one clip)
 
-fp32 on the HIP path, north_star's bar: RMS <= 1e-3 against the reference output.  The reduced-precision
-drift of config #5 (fp16, N=32832, fp32 GroupNorm statistics) over the full T=1000 loop is gated here
-against the HIP fp32 path (itself pinned to the reference above): RMS <= 2e-3.
+fp32 on the HIP path.  north_star's bar is RMS <= 1e-3; the gates here are what fp32 actually holds
+(fp32-vs-fp64 drift over T=1000 is ~1.2e-6), so an indexing or schedule slip of 1e-4
+fails.  Each loop is run twice: the graph-replayed sampler (sddm_sample, the bench's path) and the
+recording sampler (sddm_sample_continuous with sample_inter = 1), whose x_t after every step is
+compared with the fixture's intermediate x_t (every100 / every20 / every10), so a divergence is
+localised to a 10 %-of-T window.  Measured values are quoted in DESIGN.md §4.
+
+The reduced-precision drift of config #5 (fp16, N=32832, fp32 GroupNorm statistics) over the full
+T=1000 loop is gated against the HIP fp32 path (itself pinned to the reference above).
 """
 import numpy as np
 import pytest
@@ -22,15 +28,7 @@ from _helpers import diffwave_params, golden, rms, unet_config, unet_params, wav
 pytestmark = pytest.mark.gpu
 
 LONG = "long_loops.npz"
-
-
-def _unet_sample(ctx, cond_np, seed=7):
-    dev = torch.device("cuda", 0)
-    cond = torch.from_numpy(np.ascontiguousarray(cond_np)).to(dev)
-    out = torch.full_like(cond, float("nan"))
-    ctx.sample(cond, out, seed, 0)
-    torch.cuda.synchronize()
-    return out.cpu().numpy()
+GATE_FP32 = 1e-5          # RMS against the reference output and every recorded intermediate
 
 
 def _unet_ctx(N, dtype, sched):
@@ -41,65 +39,93 @@ def _unet_ctx(N, dtype, sched):
     return ctx
 
 
+def _run(ctx, cond_np, out_shape, T, seed=7):
+    """(graph-replayed x_0, recording-run x_0, recorded x_{t-1} after every step t = T..1)."""
+    dev = torch.device("cuda", 0)
+    cond = torch.from_numpy(np.ascontiguousarray(cond_np)).to(dev)
+    out = torch.full(out_shape, float("nan"), dtype=torch.float32, device=dev)
+    ctx.sample(cond, out, seed, 0)
+    out_rec = torch.full_like(out, float("nan"))
+    record = torch.full((T,) + tuple(out_shape), float("nan"), dtype=torch.float32, device=dev)
+    ctx.sample_continuous(cond, out_rec, record, 1, seed, 0)
+    torch.cuda.synchronize()
+    return out.cpu().numpy(), out_rec.cpu().numpy(), record.cpu().numpy()
+
+
+def _check(name, z, key, inter_key, every, T, out, out_rec, record):
+    ref = z[f"{key}/out"]
+    inter = z[f"{key}/{inter_key}"]                    # x_{T - every*(k+1)}: kept after step t, t % every == 1
+    err = rms(out, ref)
+    err_rec = rms(out_rec, ref)
+    steps = []
+    for k in range(inter.shape[0]):
+        t = T - every * k - (every - 1)                # the step after which the fixture kept x_{t-1}
+        steps.append((t - 1, rms(record[T - t], inter[k])))
+    worst = max(e for _, e in steps)
+    print(f"{name} fp32 vs reference: out rms {err:.3e} (recording run {err_rec:.3e}; signal rms "
+          f"{rms(ref, 0):.3f}, max |diff| {np.abs(out - ref).max():.3e}); intermediates "
+          + " ".join(f"x{t}:{e:.2e}" for t, e in steps))
+    assert out.shape == ref.shape and np.isfinite(out).all()
+    assert np.array_equal(out, out_rec), "graph-replayed and recording samplers differ"
+    for t, e in steps:
+        assert e <= GATE_FP32, f"{name}: x_{t} rms {e:.3e} > {GATE_FP32:g}"
+    assert err <= GATE_FP32 and worst <= GATE_FP32
+
+
 def test_unet_condition_in_1000_steps_matches_reference(torch_cuda):
     z = golden(LONG)
     k = "long/unet/condition_in/linear_1000_1e-06_0.001/2112x2"
-    out = _unet_sample(_unet_ctx(2112, "float32", ("linear", 1000, 1e-6, 1e-3)), z[f"{k}/cond"])
-    ref = z[f"{k}/out"]
-    err = rms(out, ref)
-    print(f"UNet T=1000 fp32 vs reference: rms {err:.3e} (signal rms {rms(ref, 0):.3f}), "
-          f"max |diff| {np.abs(out - ref).max():.3e}")
-    assert np.isfinite(out).all()
-    assert err <= 1e-3
+    ctx = _unet_ctx(2112, "float32", ("linear", 1000, 1e-6, 1e-3))
+    cond = z[f"{k}/cond"]
+    _check("UNet T=1000", z, k, "every100", 100, 1000, *_run(ctx, cond, cond.shape, 1000))
+
+
+def _spec_ctx(net, sched, hop, noise_condition="sqrt_alpha_bar"):
+    import model.diffusion as D
+    import model.model as M
+    d = D.GaussianDiffusion(*sched, device="cuda")
+    m = M.SDDM_spectrogram(d, net, hop_samples=hop, noise_condition=noise_condition).cuda()
+    return m._context(torch.device("cuda", 0))
 
 
 def test_diffwave_200_steps_matches_reference(torch_cuda):
-    import model.diffusion as D
-    import model.model as M
     import model.network as NW
     z = golden(LONG)
     k = "long/diffwave/time_step/linear_200_0.0001_0.02/63x1"
     net = NW.DiffWave(num_samples=-1, num_timesteps=200, freq_bins=513, residual_channels=64, residual_layers=30,
                       dilation_cycle_length=10)
     net.load_state_dict({n: torch.from_numpy(v) for n, v in diffwave_params().items()})
-    d = D.GaussianDiffusion("linear", 200, 1e-4, 0.02, device="cuda")
-    m = M.SDDM_spectrogram(d, net, hop_samples=256, noise_condition="time_step").cuda()
-    out = m.infer(torch.from_numpy(z[f"{k}/spec"]).cuda(), seed=7).cpu().numpy()
-    ref = z[f"{k}/out"]
-    err = rms(out, ref)
-    print(f"DiffWave T=200 fp32 vs reference: rms {err:.3e} (signal rms {rms(ref, 0):.3f})")
-    assert out.shape == ref.shape and np.isfinite(out).all()
-    assert err <= 1e-3
+    ctx = _spec_ctx(net, ("linear", 200, 1e-4, 0.02), 256, "time_step")
+    spec = z[f"{k}/spec"]
+    _check("DiffWave T=200", z, k, "every20", 20, 200, *_run(ctx, spec, (1, 1, 256 * spec.shape[-1]), 200))
 
 
 def test_wavegrad_50_steps_matches_reference(torch_cuda):
-    import model.diffusion as D
-    import model.model as M
     import model.network as NW
     z = golden(LONG)
     k = "long/wavegrad/sqrt_alpha_bar/linear_50_0.0001_0.05/54x2"
     net = NW.WaveGrad()
     net.load_state_dict({n: torch.from_numpy(v) for n, v in wavegrad_params().items()})
-    d = D.GaussianDiffusion("linear", 50, 1e-4, 0.05, device="cuda")
-    m = M.SDDM_spectrogram(d, net, hop_samples=300).cuda()
-    out = m.infer(torch.from_numpy(z[f"{k}/spec"]).cuda(), seed=7).cpu().numpy()
-    ref = z[f"{k}/out"]
-    err = rms(out, ref)
-    print(f"WaveGrad T=50 fp32 vs reference: rms {err:.3e} (signal rms {rms(ref, 0):.3f})")
-    assert out.shape == ref.shape and np.isfinite(out).all()
-    assert err <= 1e-3
+    ctx = _spec_ctx(net, ("linear", 50, 1e-4, 0.05), 300)
+    spec = z[f"{k}/spec"]
+    _check("WaveGrad T=50", z, k, "every10", 10, 50, *_run(ctx, spec, (2, 1, 300 * spec.shape[-1]), 50))
 
 
 def test_config5_fp16_drift_1000_steps(torch_cuda):
     """Config #5's arithmetic (fp16 storage, fp32 accumulation and GroupNorm statistics) over the full
-    T=1000 loop at its chunk length N=32832, 4 rows: drift against the HIP fp32 path."""
+    T=1000 loop at its chunk length N=32832, 4 rows: drift against the HIP fp32 path.  Measured 6.4e-5
+    RMS; gate 2e-4."""
     from sddm_hip.synth import noisy_speech
     N, sched = 32832, ("linear", 1000, 1e-6, 1e-3)
-    cond = noisy_speech(4, N, seed=77)
-    out32 = _unet_sample(_unet_ctx(N, "float32", sched), cond)
-    out16 = _unet_sample(_unet_ctx(N, "float16", sched), cond)
-    err = rms(out16, out32)
-    rows = [rms(out16[b], out32[b]) for b in range(4)]
+    cond = torch.from_numpy(noisy_speech(4, N, seed=77)).cuda()
+    outs = {}
+    for dt in ("float32", "float16"):
+        out = torch.full_like(cond, float("nan"))
+        _unet_ctx(N, dt, sched).sample(cond, out, 7, 0)
+        torch.cuda.synchronize()
+        outs[dt] = out.cpu().numpy()
+    err = rms(outs["float16"], outs["float32"])
+    rows = [rms(outs["float16"][b], outs["float32"][b]) for b in range(4)]
     print(f"config #5 T=1000 fp16 vs fp32 (N={N}, 4 rows): rms {err:.3e}, worst row {max(rows):.3e}")
-    assert np.isfinite(out16).all()
-    assert err <= 2e-3
+    assert np.isfinite(outs["float16"]).all()
+    assert err <= 2e-4
