@@ -80,6 +80,15 @@ int sddm_missing_params(sddm_ctx* ctx, int64_t* n_missing);
 int sddm_sample(sddm_ctx* ctx, const float* cond, int64_t B, int64_t N, uint64_t seed,
                 int64_t row_offset, float* out, void* stream);
 
+/* SURVEY.md §8(b) noise_mode 1: as sddm_sample, but every Gaussian draw comes from the caller, so the
+ * loop reproduces the reference's own torch.randn_like draws bit for bit (model.py:57-68,
+ * diffusion.py:172,187,207,220,285,306).  noise: [T + 1][B][N] fp32 device; draw 0 is x_T's noise
+ * (unused by 'supportive' and by modes starting from the condition), draw t the transition noise of
+ * step t (read for t >= 2 only).  The draws are consumed in the reference's order (x_T, then
+ * t = T .. 2), so model.model.reference_noise() stacks torch.randn_like calls into this layout. */
+int sddm_sample_noise(sddm_ctx* ctx, const float* cond, int64_t B, int64_t N, const float* noise, float* out,
+                      void* stream);
+
 /* SDDM.infer(condition, continuous=True) (model/model.py:79-103): as sddm_sample, and after the
  * step at t, whenever t % sample_inter == 0, x_{t-1} is copied to the next slot of `record`
  * ([T / sample_inter][B][N] fp32 device).  sample_inter = 1 | (T // 100) (model.py:72). */

@@ -261,6 +261,7 @@ __device__ __forceinline__ void deep_tile(const ConvArgs& a, const TembRef& te, 
   if (gn && !(a.dbg & 1)) gl.template finish<HO>(gf, b, a.CA, a.CB, gsc, gsc + Cin, hb);
   lds_sync();                                            // scale / shift visible (loads stay in flight)
   SDDM_STAMP(a, 2);
+  if (HO && hst && wv == 0) hst[0] = __builtin_amdgcn_s_memrealtime();   // team stamps (experiments)
 #pragma unroll
   for (int k = 0; k < MAXU; ++k)
 #ifdef SDDM_DEEP_GUARD
@@ -275,7 +276,7 @@ __device__ __forceinline__ void deep_tile(const ConvArgs& a, const TembRef& te, 
   }
   lds_sync();
   SDDM_STAMP(a, 3);
-  if (HO && hst && wv == 0) hst[0] = __builtin_amdgcn_s_memrealtime();   // team stamps (experiments)
+  if (HO && hst && wv == 0) hst[1] = __builtin_amdgcn_s_memrealtime();
   // bias + noise embedding of this thread's 4 epilogue channels: in flight during the K loop
   const int ec4 = (tid & (TPP - 1)) * 4;
   float bb[4], sshift;
@@ -336,7 +337,7 @@ __device__ __forceinline__ void deep_tile(const ConvArgs& a, const TembRef& te, 
     }
   }
   SDDM_STAMP(a, 4);
-  if (HO && hst && wv == 0) hst[1] = __builtin_amdgcn_s_memrealtime();
+  if (HO && hst && wv == 0) hst[2] = __builtin_amdgcn_s_memrealtime();
 
   // ---------------- 4. reduce the partial tiles: red[slot][MT][NBP] ----------------
   lds_sync();                                       // every wave is done with the image
@@ -398,7 +399,6 @@ __device__ __forceinline__ void deep_tile(const ConvArgs& a, const TembRef& te, 
     }
   }
   SDDM_STAMP(a, 5);
-  if (HO && hst && wv == 0) hst[2] = __builtin_amdgcn_s_memrealtime();
   if (a.stats && !(a.dbg & 16)) {
     // the lanes of a DPP row holding the same 4 channels (16 / TPP of them, TPP apart) add by
     // row rotations, then the 4 rows of every wave through LDS, summed by one thread per channel
@@ -473,8 +473,8 @@ __host__ __device__ constexpr int team_var(bool s2, int mt, int nb) {
   return (s2 ? 6 : 0) + (mt == 32 ? 0 : mt == 64 ? 1 : 2) * 2 + (nb == 32 ? 1 : 0);
 }
 
-template <typename T>
-__global__ __launch_bounds__(256, 2) void conv_team_kernel(TeamArgs ta, const TeamOp* __restrict__ ops) {
+template <typename T, int NW>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void conv_team_kernel(TeamArgs ta, const TeamOp* __restrict__ ops) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   __shared__ int s_ticket;
   unsigned xcc;
@@ -483,8 +483,10 @@ __global__ __launch_bounds__(256, 2) void conv_team_kernel(TeamArgs ta, const Te
   const int B = ta.B;
   const int nimg = (int)xcc < B ? (B - 1 - (int)xcc) / 8 + 1 : 0;
   if (nimg == 0) return;
-  unsigned* ticket = ta.ctr + xcc * 32;                  // one 128-byte line per team
-  unsigned* done = ta.ctr + 8 * 32;                      // [nops][B]
+  // every counter on a 256-byte slot of its own (pollers of one counter do not queue behind
+  // another's traffic): ticket of team x at slot x, done[op][b] at slot 8 + op * B + b
+  unsigned* ticket = ta.ctr + xcc * kTeamSlot;
+  unsigned* done = ta.ctr + 8 * kTeamSlot;
   // Only wave-uniform branches around the barriers of this loop: a lane-0 branch (ticket, poll,
   // publish) gets structurised into a lane-divergent loop around the barriers, which hangs (measured).
   // Wave 0 takes the ticket (its lane 0 adds 1), polls and publishes.
@@ -517,12 +519,12 @@ __global__ __launch_bounds__(256, 2) void conv_team_kernel(TeamArgs ta, const Te
       if (dep >= 0) {
         if (w0) {                                        // wave-uniform (scalar) poll loop
           const unsigned need = (unsigned)ops[dep].items;
-          unsigned* c = done + dep * B + b;
+          unsigned* c = done + (dep * B + b) * kTeamSlot;
           const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
           for (unsigned spins = 0;; ++spins) {
             const unsigned v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
             if (v >= need) break;
-            __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_s_sleep(4);                 // ~0.1 us between polls
             // 20 ms (100 MHz clock) or 2^20 polls: give up, flag it
             if (spins > (1u << 20) || __builtin_amdgcn_s_memrealtime() - t0 > 2000000ull) {
               __hip_atomic_store(ta.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -537,7 +539,7 @@ __global__ __launch_bounds__(256, 2) void conv_team_kernel(TeamArgs ta, const Te
     switch (o.var) {
 #define SDDM_TEAM_CASE(S2V, MTV, NBV)                                                                  \
   case team_var(S2V, MTV, NBV):                                                                        \
-    deep_tile<T, S2V, MTV, 4, 8, NBV, true>(o.a, te, tile, b, zb, smem, wait, ta.arena, hst);                         \
+    deep_tile<T, S2V, MTV, NW, 8, NBV, true>(o.a, te, tile, b, zb, smem, wait, ta.arena, hst);                         \
     break;
       SDDM_TEAM_CASE(false, 32, 16) SDDM_TEAM_CASE(false, 32, 32) SDDM_TEAM_CASE(false, 64, 16)
       SDDM_TEAM_CASE(false, 64, 32) SDDM_TEAM_CASE(false, 128, 16) SDDM_TEAM_CASE(false, 128, 32)
@@ -548,7 +550,7 @@ __global__ __launch_bounds__(256, 2) void conv_team_kernel(TeamArgs ta, const Te
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // every wave: its stores reached the L2
     __syncthreads();
-    if (w0) __hip_atomic_fetch_add(done + op * B + b, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (w0) __hip_atomic_fetch_add(done + (op * B + b) * kTeamSlot, one, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ta.stamps && w0 && tk < 4096) {                  // (every lane of wave 0 stores the same words)
       unsigned long long* st = ta.stamps + ((size_t)xcc * 4096 + tk) * 8;
       st[0] = (unsigned long long)op | ((unsigned long long)b << 16);
@@ -631,10 +633,17 @@ int conv_team_var(bool s2, int mt, int nb) {
   return team_var(s2, mt, nb);
 }
 
-hipError_t launch_conv_team(int dtype, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s) {
-  if (dtype == DT_F32 || lds_bytes > kTeamLdsBudget || a.nops < 1 || blocks < 8) return hipErrorInvalidValue;
-  if (dtype == DT_BF16) hipLaunchKernelGGL(conv_team_kernel<bf16_t>, dim3(blocks), dim3(256), lds_bytes, s, a, a.ops);
-  else hipLaunchKernelGGL(conv_team_kernel<f16_t>, dim3(blocks), dim3(256), lds_bytes, s, a, a.ops);
+hipError_t launch_conv_team(int dtype, int nw, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s) {
+  if (dtype == DT_F32 || lds_bytes > team_lds_budget(nw) || a.nops < 1 || blocks < 8 || (nw != 4 && nw != 8))
+    return hipErrorInvalidValue;
+  const dim3 blk(64 * nw);
+  if (dtype == DT_BF16) {
+    if (nw == 4) hipLaunchKernelGGL((conv_team_kernel<bf16_t, 4>), dim3(blocks), blk, lds_bytes, s, a, a.ops);
+    else hipLaunchKernelGGL((conv_team_kernel<bf16_t, 8>), dim3(blocks), blk, lds_bytes, s, a, a.ops);
+  } else {
+    if (nw == 4) hipLaunchKernelGGL((conv_team_kernel<f16_t, 4>), dim3(blocks), blk, lds_bytes, s, a, a.ops);
+    else hipLaunchKernelGGL((conv_team_kernel<f16_t, 8>), dim3(blocks), blk, lds_bytes, s, a, a.ops);
+  }
   return hipGetLastError();
 }
 

@@ -42,7 +42,8 @@ struct ConvInArgs {
   float* stats;               // [B][tiles][Cout][2]
   int TR;                     // frame rows per block
   int* t_dev;                 // step counter decremented once per launch (may be null)
-  unsigned* zero; int nzero;  // words cleared by the launch (team-kernel counters of the step; may be null)
+  unsigned* zero; int nzero;  // words zero[i * kTeamSlot], i < nzero, cleared by the launch (team-kernel
+                              // counters of the step; may be null)
   unsigned long long* stamps; // SDDM_STAMPS builds only
 };
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s);
@@ -113,7 +114,8 @@ struct TeamOp {
 };
 struct TeamArgs {
   const TeamOp* ops; int nops; int B;
-  unsigned* ctr;              // [8 teams][32] ticket lines, then done [nops][B]; zeroed before every launch
+  unsigned* ctr;              // counters, one per kTeamSlot words: 8 team tickets, then done [nops][B];
+                              // zeroed before every launch (conv_in, ConvInArgs::zero)
   unsigned* err;              // set to 1 when a dependency wait times out
   const float* temb; int temb_ld; const int* t_dev; int temb_per_b;
   const char* arena;          // base of the lane arena holding every activation / statistics tensor (< 4 GiB)
@@ -121,8 +123,10 @@ struct TeamArgs {
                               // {op | b << 16, s_memrealtime at ticket, after the wait, at publish,
                               //  staged, K loop done, stored, statistics written}
 };
-constexpr int kTeamLdsBudget = 80 * 1024;    // two 4-wave workgroups per CU
-hipError_t launch_conv_team(int dtype, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s);
+// nw = 4: two 4-wave workgroups per CU (64 per XCD); nw = 8: one 8-wave workgroup per CU (32 per XCD)
+constexpr int team_lds_budget(int nw) { return nw == 8 ? 160 * 1024 : 80 * 1024; }
+constexpr int kTeamSlot = 64;                 // words per team counter (256 bytes)
+hipError_t launch_conv_team(int dtype, int nw, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s);
 int conv_team_var(bool s2, int mt, int nb);  // -1: no team variant for this tiling
 
 // ---- row-streaming 3x3 convolution for segment widths 64 / 128 (conv_strip.hip) ----
@@ -152,18 +156,24 @@ struct FinalArgs {
   TransCoef co;
   uint64_t seed; int64_t row_offset;
   const StepParams* sp;       // when set, seed / row_offset come from device memory (graph replay)
+  const float* noise; int64_t noise_ld;   // caller-supplied draws (TransArgs), row b of draw t at noise[t * noise_ld + b * N]
   unsigned long long* stamps; // SDDM_STAMPS builds only
 };
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s);
 
 // ---- standalone transition / initial state (diffusion.py:164-223, 281-320; model.py:57-68) ----
+// noise (nullable): caller-supplied standard-normal draws [draw][noise_ld] (sddm_sample_noise): draw 0 is
+// x_T's, draw t the transition's at step t, element i of a draw at noise[draw * noise_ld + i] (i = the
+// call-local flat index); null = the Philox stream keyed by (seed, draw, global element)
 struct TransArgs {
   int mode; const float* x_t; const float* eps; const float* cond; float* out;
   int64_t total; int64_t N; int t; const int* t_dev; TransCoef co; uint64_t seed; int64_t row_offset;
+  const float* noise; int64_t noise_ld;
 };
 hipError_t launch_transition(const TransArgs& a, hipStream_t s);
 struct InitArgs {
   int mode; const float* cond; float* out; int64_t total; int64_t N; int T; TransCoef co; uint64_t seed; int64_t row_offset;
+  const float* noise;         // caller-supplied draw 0 (nullable), element i at noise[i]
 };
 hipError_t launch_init_state(const InitArgs& a, hipStream_t s);
 hipError_t launch_set_int(int* p, int v, hipStream_t s);

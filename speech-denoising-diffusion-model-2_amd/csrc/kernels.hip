@@ -148,7 +148,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   // zero the step's team-kernel counters (ticket lines + completion counters, conv_deep.hip): the
   // team launch later in this step finds them zero (kernel boundary in between)
   if (a.zero && blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = tid; i < a.nzero; i += 256) a.zero[i] = 0u;
+    for (int i = tid; i < a.nzero; i += 256) a.zero[(size_t)i * kTeamSlot] = 0u;
   SDDM_STAMP(a, 0);
   const int S = a.S, F = a.F, W = a.W, IW = W + 2, IH = a.TR + 2;
   {  // every load of the frame image issued before the first is stored (clamped addresses:
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(256) void transition_kernel(TransArgs a) {
   const bool needs_cond = a.mode >= 2;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.total; i += (int64_t)gridDim.x * blockDim.x) {
     const uint64_t e = (uint64_t)(a.row_offset * a.N + i);
-    const float z = t > 1 ? philox_normal1(a.seed, (uint32_t)t, e) : 0.f;
+    const float z = t > 1 ? (a.noise ? a.noise[(int64_t)t * a.noise_ld + i] : philox_normal1(a.seed, (uint32_t)t, e)) : 0.f;
     a.out[i] = transition_one(a.mode, a.co, t, a.x_t[i], a.eps[i], needs_cond ? a.cond[i] : 0.f, z);
   }
 }
@@ -344,7 +344,7 @@ __global__ __launch_bounds__(256) void init_state_kernel(InitArgs a) {
     if (a.mode == 2) {
       v = a.cond[i];                                              // supportive: x_T = condition
     } else {
-      const float z = philox_normal1(a.seed, 0u, e);
+      const float z = a.noise ? a.noise[i] : philox_normal1(a.seed, 0u, e);
       if (a.mode == 4) {                                          // condition_in: get_x_T
         const float s = a.co.sqrt_alpha_bar[T];
         v = s * a.cond[i] + sqrtf(1.0f - s * s) * z;
@@ -506,7 +506,8 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
     const uint64_t e0 = (uint64_t)(ebase + n4);
     f32x4 z = {0.f, 0.f, 0.f, 0.f};
     const bool aligned = (e0 & 3) == 0;
-    if (a.mode >= 0 && t > 1 && aligned) z = philox_normal4(seed, (uint32_t)t, e0 >> 2);
+    if (a.mode >= 0 && t > 1 && a.noise) z = *(const f32x4*)(a.noise + (int64_t)t * a.noise_ld + (int64_t)b * a.N + n4);
+    else if (a.mode >= 0 && t > 1 && aligned) z = philox_normal4(seed, (uint32_t)t, e0 >> 2);
     f32x4 e4 = {0.f, 0.f, 0.f, 0.f};
     if ((S & 3) == 0 && (W & 3) == 0) {
       // overlapAdd of 4 consecutive samples: with S and W multiples of 4 they are covered by the
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
       f32x4 o;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float zz = (t > 1) ? (aligned ? z[j] : philox_normal1(seed, (uint32_t)t, e0 + j)) : 0.f;
+        const float zz = (t > 1) ? ((aligned || a.noise) ? z[j] : philox_normal1(seed, (uint32_t)t, e0 + j)) : 0.f;
         o[j] = transition_one(a.mode, a.co, t, xin[j], e4[j], a.cond ? cin[j] : 0.f, zz);
       }
       if (n4 + 3 < n_end) *(f32x4*)(xrow + n4) = o;

@@ -224,6 +224,8 @@ struct RunState {  // fields patched into the plan's kernel arguments at launch 
   float* eps_out = nullptr;
   uint64_t seed = 0;
   int64_t row_offset = 0;
+  const float* noise = nullptr;   // caller-supplied draws of this lane's rows (sddm_sample_noise), or null
+  int64_t noise_ld = 0;
 };
 
 static constexpr int kTeamDefault = 0;  // deep-level team kernel off until it beats the per-layer launches
@@ -565,7 +567,7 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
 // items x one item's latency: its L2 bytes at ~64 B/clk into one CU + its MFMA cycles + a fixed
 // ~1500 clk of hand-off and round trips) and the team's L2 bytes at ~2 KB/clk.  SDDM_TEAM_CFG=mt:nb
 // forces a tiling wherever it fits (experiments).
-static bool choose_team(int dt, int PB, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
+static bool choose_team(int dt, int PB, int nw, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
                         ConvChoice& ch) {
   static int f_mt = -1, f_nb = 0;
   if (f_mt < 0) {
@@ -576,32 +578,34 @@ static bool choose_team(int dt, int PB, int Cin, int RC, int res_mode, int Ho, i
   ConvArgs a{};
   a.CA = Cin; a.RCA = RC; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.upsample = up ? 1 : 0;
   a.Hi = up ? Ho / 2 : (s2 ? Ho * 2 : Ho); a.Wi = up ? Wo / 2 : (s2 ? Wo * 2 : Wo);
-  a.deep_nw = 4;
+  a.deep_nw = nw;
   const int nimg = (PB + 7) / 8, es = 2, K = 9 * Cin + (res_mode == 2 ? RC : 0);
+  const double wgs = 32.0 * 8 / nw;              // workgroups of a team
   double best = 1e30;
   bool found = false;
   for (int mt : {32, 64, 128})
     for (int nb : {16, 32}) {
       if (conv_team_var(s2, mt, nb) < 0 || Cout % nb) continue;
+      if (nw == 8 && s2 && nb == 16) continue;     // no per-layer conv_deep of that shape (team mode 2 reference)
       if (f_mt && (mt != f_mt || nb != f_nb)) continue;
       const int TW = std::min(Wo, mt);
       if (mt % TW || Wo % TW) continue;
       const int TR = std::min(mt / TW, Ho);
       if (Ho % TR || (TR * TW < mt && mt > 32)) continue;
       a.TR = TR; a.TW = TW; a.tiles_x = Wo / TW; a.n_tiles = a.tiles_x * (Ho / TR); a.deep_nb = nb;
-      if (conv_deep_lds_bytes(dt, mt, s2, a) > (size_t)kTeamLdsBudget) continue;
+      if (conv_deep_lds_bytes(dt, mt, s2, a) > (size_t)team_lds_budget(nw)) continue;
       const double halo = s2 ? (2.0 * TR + 1) * (2 * TW + 1) : (TR + 2.0) * (TW + 2);
       const double item_bytes = (double)nb * K * es + halo * Cin * es + (res_mode == 2 ? (double)TR * TW * RC * es : 0) +
                                 (double)TR * TW * nb * es * (res_mode == 1 ? 2 : 1);
       const double items = (double)a.n_tiles * (Cout / nb) * nimg;
       const double mfma = (mt / 16.0) * (nb / 16.0) * (K / 32.0) * 8.0 / 4.0;
-      const double rounds = std::ceil(items / 64.0);
+      const double rounds = std::ceil(items / wgs);
       const double cost = std::max(rounds * (item_bytes / 64.0 + mfma + 1500.0), items * item_bytes / 2048.0);
       if (cost < best) {
         best = cost;
         found = true;
         ch = ConvChoice{};
-        ch.strip = 0; ch.mt = mt; ch.nw = 4; ch.nb = nb; ch.ckb = Cin / 32; ch.team = 1;
+        ch.strip = 0; ch.mt = mt; ch.nw = nw; ch.nb = nb; ch.ckb = Cin / 32; ch.team = 1;
         ch.TR = TR; ch.TW = TW; ch.tiles_x = a.tiles_x; ch.n_tiles = a.n_tiles;
       }
     }
@@ -763,6 +767,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   const int team_mode = env_team ? std::atoi(env_team) : c->team;
   const bool team_on = dt != DT_F32 && team_mode != 0 && (env_team != nullptr || PB >= 8);
   const int team_px = env_team_px > 0 ? env_team_px : c->team_px;
+  static const int team_nw = std::getenv("SDDM_TEAM_NW") ? std::atoi(std::getenv("SDDM_TEAM_NW")) : 8;
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
     int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;
@@ -775,7 +780,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         if (kind == 3) { wm = kt->second.a; wn = kt->second.b; wb = kt->second.c; }
       }
     }
-    if (team_on && Ho * Wo <= team_px && choose_team(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch)) return true;
+    if (team_on && Ho * Wo <= team_px && choose_team(dt, PB, team_nw, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch)) return true;
     return choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka, wb);
   };
   const int TRin = 512 / W;
@@ -857,7 +862,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         tp.steps.assign(prog.begin() + i, prog.begin() + j);
         tp.off_ops = A.reserve(sizeof(TeamOp) * tp.steps.size());
         tp.ctr_word = (size_t)n_ctr;
-        n_ctr += 8 * 32 + (int)tp.steps.size() * B;
+        n_ctr += 8 + (int)tp.steps.size() * B;            // counters (kTeamSlot words each)
         Step ts;
         ts.type = ST_TEAM;
         ts.team = (int)teams.size();
@@ -873,7 +878,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
     prog.swap(np);
     if (!teams.empty()) {
       off_err = A.reserve(256);
-      off_ctr = A.reserve(sizeof(unsigned) * (size_t)n_ctr);
+      off_ctr = A.reserve(sizeof(unsigned) * kTeamSlot * (size_t)n_ctr);
     }
   }
   SDDM_HIP_CHECK(A.commit());
@@ -1049,7 +1054,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         double by = 0, fl = 0;
         if (const int r = conv_args(ms, o.a, by, fl)) return r;
         bytes += by; flops += fl;
-        o.a.deep_nw = 4; o.a.deep_nb = ms.ch.nb; o.a.ck_batch = ms.ch.ckb;
+        o.a.deep_nw = ms.ch.nw; o.a.deep_nb = ms.ch.nb; o.a.ck_batch = ms.ch.ckb;
         o.var = conv_team_var(ms.s2 != 0, ms.ch.mt, ms.ch.nb);
         if (o.var < 0) FAIL(SDDM_ERR_STATE, "no team variant for %s", ms.w.c_str());
         o.items = o.a.n_tiles * (o.a.Cout / ms.ch.nb);
@@ -1063,12 +1068,13 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                   ms.w.c_str(), ms.ch.mt, ms.ch.nb, o.a.n_tiles, o.items, o.a.CA + o.a.CB, o.a.Cout, o.a.gtilesA,
                   o.a.gtilesB, conv_deep_lds_bytes(dt, ms.ch.mt, ms.s2 != 0, o.a));
       }
-      if (lds > kTeamLdsBudget) FAIL(SDDM_ERR_STATE, "team LDS %d bytes", lds);
+      const int tnw = tp.steps.front().ch.nw;
+      if (lds > team_lds_budget(tnw)) FAIL(SDDM_ERR_STATE, "team LDS %d bytes", lds);
       SDDM_HIP_CHECK(hipMemcpy(A.base + tp.off_ops, ops.data(), sizeof(TeamOp) * ops.size(), hipMemcpyHostToDevice));
       SDDM_HIP_CHECK(hipMemset(A.base + off_err, 0, 256));
       TeamArgs ta{};
       ta.ops = A.at<TeamOp>(tp.off_ops); ta.nops = (int)ops.size(); ta.B = B;
-      ta.ctr = A.at<unsigned>(off_ctr) + tp.ctr_word; ta.err = A.at<unsigned>(off_err);
+      ta.ctr = A.at<unsigned>(off_ctr) + tp.ctr_word * kTeamSlot; ta.err = A.at<unsigned>(off_err);
       ta.arena = (const char*)A.base;
       if (std::getenv("SDDM_TEAM_STAMPS")) {   // per-item timestamps (experiments; sddm_debug_stamps)
         if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
@@ -1076,15 +1082,15 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         ta.stamps = c->stamp_buf;
         c->stamp_blocks = 8 * 4096;          // [8 teams][4096 tickets][8 words]
       }
-      const int blocks = 8 * 64;       // two 4-wave workgroups on each of an XCD's 32 CUs
+      const int blocks = 8 * 32 * 8 / tnw;   // 4 waves: two workgroups on each of an XCD's 32 CUs; 8 waves: one
       const std::string nm = "team[" + tp.steps.front().w + ".." + tp.steps.back().w + "]";
-      L.ops.push_back({2, bytes, flops, [ctx, lp, ta, lds, blocks, dt](hipStream_t s) {
+      L.ops.push_back({2, bytes, flops, [ctx, lp, ta, lds, blocks, dt, tnw](hipStream_t s) {
                           TeamArgs x = ta;
                           x.temb = lp->rs.temb; x.temb_ld = ctx->SC; x.t_dev = lp->rs.t_dev;
                           x.temb_per_b = lp->rs.temb_per_b;
-                          return launch_conv_team(dt, x, lds, blocks, s);
+                          return launch_conv_team(dt, tnw, x, lds, blocks, s);
                         }, nm});
-      L.ops.back().kname = std::string("conv_team_kernel<") + dt_name(dt) + ">";
+      L.ops.back().kname = std::string("conv_team_kernel<") + dt_name(dt) + "," + std::to_string(tnw) + ">";
       L.ops.back().kinst = L.ops.back().kname;
       L.team_err = ta.err;
     } else {
@@ -1118,6 +1124,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           x.mode = lp->rs.final_mode; x.eps_out = lp->rs.eps_out;
                           x.x = lp->rs.x; x.cond = lp->rs.cond; x.t_dev = lp->rs.t_dev;
                           x.seed = lp->rs.seed; x.row_offset = lp->rs.row_offset;
+                          x.noise = lp->rs.noise; x.noise_ld = lp->rs.noise_ld;
                           x.sp = lp->rs.t_dev ? (const StepParams*)lp->rs.t_dev : nullptr;
                           return launch_final(dt, x, B, s);
                         }, "final_conv"});
@@ -1503,11 +1510,17 @@ static int prepare_plan(sddm_ctx* c, int64_t B, int64_t N) {
 }
 
 static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed, int64_t row_offset,
-                       float* out, float* record, int sample_inter, void* stream);
+                       float* out, float* record, int sample_inter, void* stream, const float* noise = nullptr);
 
 int sddm_sample(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed, int64_t row_offset,
                 float* out, void* stream) {
   return sample_impl(c, cond, B, N, seed, row_offset, out, nullptr, 0, stream);
+}
+
+int sddm_sample_noise(sddm_ctx* c, const float* cond, int64_t B, int64_t N, const float* noise, float* out,
+                      void* stream) {
+  if (!noise) FAIL(SDDM_ERR_INVALID_ARG, "NULL noise");
+  return sample_impl(c, cond, B, N, 0, 0, out, nullptr, 0, stream, noise);
 }
 
 int sddm_sample_continuous(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed,
@@ -1517,16 +1530,17 @@ int sddm_sample_continuous(sddm_ctx* c, const float* cond, int64_t B, int64_t N,
 }
 
 static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uint64_t seed, int64_t row_offset,
-                       float* out, float* record, int sample_inter, void* stream) {
+                       float* out, float* record, int sample_inter, void* stream, const float* noise) {
   int r = ensure_ready(c);
   if (r) return r;
   if (!cond || !out) FAIL(SDDM_ERR_INVALID_ARG, "NULL tensor");
-  if (c->dws) return dw_sample(c, cond, B, N, seed, row_offset, out, record, sample_inter, (hipStream_t)stream);
-  if (c->wgs) return wg_sample(c, cond, B, N, seed, row_offset, out, record, sample_inter, (hipStream_t)stream);
+  if (c->dws) return dw_sample(c, cond, B, N, seed, row_offset, out, record, sample_inter, noise, (hipStream_t)stream);
+  if (c->wgs) return wg_sample(c, cond, B, N, seed, row_offset, out, record, sample_inter, noise, (hipStream_t)stream);
   r = prepare_plan(c, B, N);
   if (r) return r;
   hipStream_t user = (hipStream_t)stream;
-  const bool graph = c->use_graphs && !c->prof && !record;
+  // (caller-supplied noise: the step graphs would bake its pointer; the per-launch path reads it)
+  const bool graph = c->use_graphs && !c->prof && !record && !noise;
   const int T = c->T;
   StepParams* sp0 = c->warena.at<StepParams>(c->off_tdev);
   float* temb_tab = c->warena.at<float>(c->off_temb_tab);
@@ -1554,10 +1568,12 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
     InitArgs ia{};
     ia.mode = c->init_mode; ia.cond = cb; ia.out = xb; ia.total = rows * N; ia.N = N; ia.T = T;
     ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset + L.row0;
+    ia.noise = noise ? noise + off : nullptr;
     SDDM_HIP_CHECK(launch_init_state(ia, user));
     SDDM_HIP_CHECK(launch_set_params(sp, T + 1, seed, row_offset + L.row0, user));
     L.rs.cond = cb; L.rs.x = xb; L.rs.temb = temb_tab; L.rs.temb_per_b = 0; L.rs.t_dev = &sp->t;
     L.rs.final_mode = c->tr_mode; L.rs.eps_out = nullptr; L.rs.seed = seed; L.rs.row_offset = row_offset + L.row0;
+    L.rs.noise = noise ? noise + off : nullptr; L.rs.noise_ld = B * N;
   }
   if (graph) {
     const int ns = std::min<int>(kStreams, (int)c->lanes.size());
@@ -1648,6 +1664,7 @@ int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const
     SDDM_HIP_CHECK(launch_embed(e, s));
     L.rs.cond = cond + off; L.rs.x = const_cast<float*>(x_t) + off; L.rs.temb = temb; L.rs.temb_per_b = 1;
     L.rs.t_dev = nullptr; L.rs.final_mode = -1; L.rs.eps_out = eps_out + off; L.rs.seed = 0; L.rs.row_offset = 0;
+    L.rs.noise = nullptr;
     r = run_ops(c, L, s);
     if (r) return r;
   }

@@ -331,7 +331,7 @@ static int wg_check_shape(sddm_ctx* c, int64_t B, int64_t N, int* F) {
 
 // SDDM_spectrogram.infer (model.py:212-257) with WaveGrad: spec [B][128][F], out [B][1][300 F]
 static int wg_sample(sddm_ctx* c, const float* spec, int64_t B, int64_t N, uint64_t seed, int64_t row_offset, float* out,
-                     float* record, int sample_inter, hipStream_t s) {
+                     float* record, int sample_inter, const float* noise, hipStream_t s) {
   WGState& d = *c->wgs;
   int F = 0;
   WG_TRY(wg_check_shape(c, B, N, &F));
@@ -342,7 +342,7 @@ static int wg_sample(sddm_ctx* c, const float* spec, int64_t B, int64_t N, uint6
   WG_TRY(wg_condition(c, spec, (int)B, F, s));
   InitArgs ia{};                                       // x_T = randn(B, 1, hop F) (model.py:216)
   ia.mode = 0; ia.cond = nullptr; ia.out = out; ia.total = B * N; ia.N = N; ia.T = T;
-  ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset;
+  ia.co = c->coef(); ia.seed = seed; ia.row_offset = row_offset; ia.noise = noise;
   SDDM_HIP_CHECK(launch_init_state(ia, s));
   StepParams* sp = c->warena.at<StepParams>(d.off_sp);
   SDDM_HIP_CHECK(launch_set_params(sp, T + 1, seed, row_offset, s));
@@ -353,6 +353,7 @@ static int wg_sample(sddm_ctx* c, const float* spec, int64_t B, int64_t N, uint6
     TransArgs ta{};                                    // p_transition (diffusion.py:177-190)
     ta.mode = SDDM_TR_ORIGINAL; ta.x_t = out; ta.eps = eps; ta.cond = nullptr; ta.out = out;
     ta.total = B * N; ta.N = N; ta.t = t; ta.t_dev = &sp->t; ta.co = c->coef(); ta.seed = seed; ta.row_offset = row_offset;
+    ta.noise = noise; ta.noise_ld = B * N;
     SDDM_HIP_CHECK(launch_transition(ta, s));
     if (record && t % sample_inter == 0) {
       SDDM_HIP_CHECK(hipMemcpyAsync(record + nrec * B * N, out, sizeof(float) * B * N, hipMemcpyDeviceToDevice, s));

@@ -8,6 +8,9 @@ returns x_0.  Extra keyword arguments (all optional, defaults keep the reference
   seed        noise-stream seed; default draws one from torch's CPU generator
   row_offset  global index of this batch's first row (multi-GPU sharding: rows keep the
               same noise whatever rank samples them)
+  noise       caller-supplied Gaussian draws [T + 1, *x_T.shape] (SURVEY §8(b) noise_mode 1) in place
+              of the device Philox stream; reference_noise() draws them with torch exactly as the
+              reference's infer does, so the output matches the reference run from the same torch seed
   compute_dtype (constructor / attribute): 'float32' (parity, default), 'bfloat16', 'float16'
   lane_rows   (attribute): rows per lane of the UNet plan (library default 16; 64 for per-GPU
               batches of 64+ rows, e.g. config #5)
@@ -107,14 +110,19 @@ class SDDM(nn.Module):
         return predicted, noise
 
     @torch.no_grad()
-    def infer(self, condition, continuous=False, seed=None, row_offset=0):
+    def infer(self, condition, continuous=False, seed=None, row_offset=0, noise=None):
         """Reverse diffusion x_T -> x_0 (model.py:50-124).  condition: [B, 1, N] on the HIP device."""
         if not condition.is_cuda:
             raise RuntimeError("SDDM.infer runs on the HIP device; move the condition to cuda")
         cond = condition.contiguous().float()
         ctx = self._context(cond.device)
-        seed = _seed_from_torch() if seed is None else int(seed)
         out = torch.empty_like(cond)
+        if noise is not None:
+            if continuous:
+                raise NotImplementedError("caller-supplied noise with continuous sampling")
+            ctx.sample_noise(cond, out, _noise_buffer(noise, self.num_timesteps, out))
+            return out
+        seed = _seed_from_torch() if seed is None else int(seed)
         if not continuous:
             ctx.sample(cond, out, seed, row_offset)
             return out
@@ -135,7 +143,7 @@ class SDDM_spectrogram(SDDM):
         self.hop_samples = hop_samples
 
     @torch.no_grad()
-    def infer(self, condition, continuous=False, seed=None, row_offset=0):
+    def infer(self, condition, continuous=False, seed=None, row_offset=0, noise=None):
         """Reverse diffusion from x_T = randn(B, 1, hop * F) (model.py:212-257).
         condition: spectrogram [B, bins, F] on the HIP device -> [B, 1, hop * F]."""
         if not condition.is_cuda:
@@ -146,9 +154,14 @@ class SDDM_spectrogram(SDDM):
             raise RuntimeError(f"{type(self.noise_estimate_model).__name__} expects a spectrogram condition "
                                f"[B, {bins}, frames], got {tuple(spec.shape)}")
         ctx = self._context(spec.device)
-        seed = _seed_from_torch() if seed is None else int(seed)
         B = spec.shape[0]
         out = torch.empty((B, 1, self.hop_samples * spec.shape[-1]), dtype=torch.float32, device=spec.device)
+        if noise is not None:
+            if continuous:
+                raise NotImplementedError("caller-supplied noise with continuous sampling")
+            ctx.sample_noise(spec, out, _noise_buffer(noise, self.num_timesteps, out))
+            return out
+        seed = _seed_from_torch() if seed is None else int(seed)
         if not continuous:
             ctx.sample(spec, out, seed, row_offset)
             return out
@@ -158,6 +171,35 @@ class SDDM_spectrogram(SDDM):
         record = torch.empty((max(nrec, 1),) + tuple(out.shape), dtype=torch.float32, device=spec.device)
         ctx.sample_continuous(spec, out, record, inter, seed, row_offset)
         return [condition] + [record[i] for i in range(nrec)]
+
+
+def _noise_buffer(noise, T, out):
+    """Caller noise as the contiguous fp32 [T + 1][B][N] device buffer of sddm_sample_noise."""
+    n = torch.as_tensor(noise)
+    if n.shape[0] != T + 1 or n[0].numel() != out.numel():
+        raise ValueError(f"noise must be [T + 1 = {T + 1}, {tuple(out.shape)}], got {tuple(n.shape)}")
+    return n.to(device=out.device, dtype=torch.float32).contiguous()
+
+
+def reference_noise(model, condition, device=None, generator=None):
+    """The standard-normal draws the reference's infer makes, in its order, as [T + 1, *x_T.shape]:
+    slot 0 = x_T's draw (SDDM: get_x_T / get_x_T_conditional / randn_like, none for 'supportive',
+    model.py:57-68; SDDM_spectrogram: torch.randn(B, 1, hop F), model.py:216), slot t = the
+    p_transition* draw of step t for t = T .. 2 (diffusion.py:172,187,207,220).  Drawn with
+    torch.randn on `device` (default: the condition's, as the reference) from `generator` (default:
+    that device's default generator), so seeding torch as a reference run did reproduces its noise."""
+    T = model.num_timesteps
+    device = condition.device if device is None else torch.device(device)
+    if hasattr(model, "hop_samples"):
+        shape = (condition.shape[0], 1, model.hop_samples * condition.shape[-1])
+    else:
+        shape = tuple(condition.shape)
+    out = torch.zeros((T + 1,) + shape, dtype=torch.float32)
+    if hasattr(model, "hop_samples") or model.p_transition != "supportive":
+        out[0] = torch.randn(shape, device=device, generator=generator).cpu()
+    for t in range(T, 1, -1):
+        out[t] = torch.randn(shape, device=device, generator=generator).cpu()
+    return out
 
 
 # ---------------------------------------------------------------------------------------------

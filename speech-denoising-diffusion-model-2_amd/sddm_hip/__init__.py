@@ -23,7 +23,7 @@ TABLE_NAMES = ("betas", "alphas", "alpha_bar", "sqrt_alpha_bar", "predicted_nois
                "supportive_gamma", "supportive_sigma_hat", "m", "sqrt_delta", "c_xt", "c_yt", "c_epst",
                "sqrt_delta_estimated")
 EXPORTS = ("sddm_abi_version", "sddm_last_error", "sddm_create", "sddm_destroy", "sddm_configure",
-           "sddm_load_param", "sddm_missing_params", "sddm_sample", "sddm_sample_continuous",
+           "sddm_load_param", "sddm_missing_params", "sddm_sample", "sddm_sample_noise", "sddm_sample_continuous",
            "sddm_network_forward",
            "sddm_transition", "sddm_q_sample", "sddm_log_spectrogram", "sddm_set_conv_tuning", "sddm_initial_state", "sddm_schedule", "sddm_profile_enable",
            "sddm_profile_read", "sddm_profile_ops")
@@ -49,6 +49,7 @@ def lib():
         L.sddm_load_param.argtypes = [vp, ctypes.c_char_p, vp, ctypes.POINTER(i64), c_int, c_int]
         L.sddm_missing_params.argtypes = [vp, ctypes.POINTER(i64)]
         L.sddm_sample.argtypes = [vp, vp, i64, i64, u64, i64, vp, vp]
+        L.sddm_sample_noise.argtypes = [vp, vp, i64, i64, vp, vp, vp]
         L.sddm_sample_continuous.argtypes = [vp, vp, i64, i64, u64, i64, vp, vp, c_int, vp]
         L.sddm_network_forward.argtypes = [vp, vp, vp, vp, i64, i64, vp, vp]
         L.sddm_transition.argtypes = [vp, c_int, vp, vp, vp, c_int, i64, i64, u64, i64, vp, vp]
@@ -147,6 +148,12 @@ class Context:
         B, N = out.shape[0], out.shape[-1]          # spectrogram archs: cond is [B, bins, frames]
         check(lib().sddm_sample(self._h, _ptr(cond), B, N, int(seed) & (2 ** 64 - 1), int(row_offset),
                                 _ptr(out), _stream(torch, cond.device)))
+
+    def sample_noise(self, cond, out, noise):
+        """sddm_sample_noise: every Gaussian draw from `noise` ([T + 1][B][N] fp32 on the device)."""
+        import torch
+        B, N = out.shape[0], out.shape[-1]
+        check(lib().sddm_sample_noise(self._h, _ptr(cond), B, N, _ptr(noise), _ptr(out), _stream(torch, cond.device)))
 
     def sample_continuous(self, cond, out, record, sample_inter, seed, row_offset=0):
         import torch

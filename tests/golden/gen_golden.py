@@ -66,7 +66,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reference", default="/root/reference")
     ap.add_argument("--out", default=HERE)
-    ap.add_argument("--only", default=None, help="regenerate one fixture group (wavegrad)")
+    ap.add_argument("--only", default=None, help="regenerate one fixture group (stft, q, wavegrad, long, torchnoise)")
     args = ap.parse_args()
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "speech-denoising-diffusion-model-2_amd"))
@@ -94,6 +94,9 @@ def main():
         return
     if args.only == "long":
         gen_long(torch, philox, make_params, GaussianDiffusion, noisy_speech, args.out)
+        return
+    if args.only == "torchnoise":
+        gen_torchnoise(torch, make_params, GaussianDiffusion, noisy_speech, args.out)
         return
 
     # 1. schedule tables (diffusion.py:50-161)
@@ -357,6 +360,47 @@ def gen_wavegrad(torch, philox, make_params, GaussianDiffusion, out_dir):
     keys["wavegrad"] = [[k, list(v.shape)] for k, v in net.state_dict().items()]
     with open(os.path.join(out_dir, "state_dict_keys.json"), "w") as f:
         json.dump(keys, f, indent=0)
+
+
+def gen_torchnoise(torch, make_params, GaussianDiffusion, noisy_speech, out_dir):
+    """12. sampling loops with the reference's OWN noise (torch_noise.npz): no injection, torch seeded
+    with torch.manual_seed(seed) right before infer, so every draw is the reference's torch.randn_like /
+    torch.randn on the CPU generator (model.py:57-68,216; diffusion.py:172,187,207,220,285,306).
+    The HIP side replays the same draws through sddm_sample_noise (SURVEY §8(b) noise_mode 1)."""
+    from model.UNetModified2 import UNetModified2
+    from model.model import SDDM, SDDM_spectrogram
+    from model.diffwave import DiffWave
+    from model.wavegrad import WaveGrad
+    tn = {}
+    sched, N, B = ("linear", 6, 1e-4, 0.05), 2112, 2
+    net = UNetModified2(num_samples=N, **UNET_ARGS)
+    P = make_params({k: tuple(v.shape) for k, v in net.state_dict().items()}, 0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    cond = noisy_speech(B, N, seed=4321)
+    for i, mode in enumerate(("condition_in", "original", "sr3", "supportive", "conditional")):
+        d = GaussianDiffusion(*sched, device="cpu")
+        m = SDDM(d, net, p_transition=mode).eval()
+        seed = 100 + i
+        torch.manual_seed(seed)
+        with torch.no_grad():
+            y = m.infer(torch.from_numpy(cond))
+        key = f"torchnoise/unet/{mode}/{sched_key(sched)}/{N}x{B}"
+        tn[key + "/cond"], tn[key + "/out"], tn[key + "/seed"] = cond, y.numpy().copy(), np.array(seed)
+    sched, F = ("linear", 6, 1e-4, 0.02), 16
+    net = DiffWave(num_samples=-1, num_timesteps=sched[1], freq_bins=513, residual_channels=64, residual_layers=30,
+                   dilation_cycle_length=10)
+    P = make_params({k: tuple(v.shape) for k, v in net.state_dict().items()}, 0)
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    m = SDDM_spectrogram(GaussianDiffusion(*sched, device="cpu"), net, hop_samples=256,
+                         noise_condition="time_step").eval()
+    spec = np.random.default_rng(5).uniform(0, 1, (1, 513, F)).astype(np.float32)
+    torch.manual_seed(200)
+    with torch.no_grad():
+        y = m.infer(torch.from_numpy(spec))
+    key = f"torchnoise/diffwave/time_step/{sched_key(sched)}/{F}x1"
+    tn[key + "/spec"], tn[key + "/out"], tn[key + "/seed"] = spec, y.numpy().copy(), np.array(200)
+    np.savez_compressed(os.path.join(out_dir, "torch_noise.npz"), **tn)
+    print("wrote", os.path.join(out_dir, "torch_noise.npz"))
 
 
 def gen_long(torch, philox, make_params, GaussianDiffusion, noisy_speech, out_dir):

@@ -53,7 +53,7 @@ def main():
     t0 = st[:, 1].min()
     ops = (st[:, 0] & 0xFFFF).astype(int)
     print(f"{len(st)} items, launch span {(st[:, 3].max() - t0) / 100:.1f} us")
-    print(" op  items  first-ticket  last-publish  span   mean-wait  item: stage  kloop  store  stats  publish (us after the wait)")
+    print(" op  items  first-ticket  last-publish  span   mean-wait  item: gnfin  staged kloop  stats  publish (us after the wait)")
     prev_end = 0.0
     for o in sorted(set(ops)):
         m = st[ops == o]
