@@ -58,11 +58,12 @@ def transition(mode, tab, x_t, t, eps, cond=None, noise=None):
     return np.clip(x.astype(np.float32), f32(-1.0), f32(1.0))
 
 
-def initial_state(mode, tab, cond, seed, row_offset=0):
-    """x_T per SDDM.infer (model/model.py:57-68)."""
+def initial_state(mode, tab, cond, seed, row_offset=0, z=None):
+    """x_T per SDDM.infer (model/model.py:57-68); z = the x_T draw (default: Philox draw 0)."""
     if mode == "supportive":
         return cond.astype(np.float32).copy()
-    z = philox.normal(seed, 0, cond.shape, row_offset)
+    if z is None:
+        z = philox.normal(seed, 0, cond.shape, row_offset)
     if mode == "conditional":
         return get_x_T_conditional(tab, cond, z)
     if mode == "condition_in":
@@ -71,11 +72,12 @@ def initial_state(mode, tab, cond, seed, row_offset=0):
 
 
 def infer(network, tab, cond, mode="condition_in", noise_condition="sqrt_alpha_bar", seed=7,
-          row_offset=0, record=None):
-    """SDDM.infer (model/model.py:50-124): ``network(cond, x_t, noise_level[B]) -> eps``."""
+          row_offset=0, record=None, noise=None):
+    """SDDM.infer (model/model.py:50-124): ``network(cond, x_t, noise_level[B]) -> eps``.
+    noise: optional [T + 1, *cond.shape] draws (slot 0 = x_T, slot t = step t) in place of Philox."""
     T = len(tab["betas"]) - 1
     B = cond.shape[0]
-    x = initial_state(mode, tab, cond, seed, row_offset)
+    x = initial_state(mode, tab, cond, seed, row_offset, None if noise is None else noise[0])
     if record is not None:
         record.append(x.copy())
     for t in range(T, 0, -1):
@@ -84,7 +86,7 @@ def infer(network, tab, cond, mode="condition_in", noise_condition="sqrt_alpha_b
         else:
             nl = np.full(B, float(t), dtype=np.float32)
         eps = network(cond, x, nl)
-        z = philox.normal(seed, t, x.shape, row_offset) if t > 1 else None
+        z = (philox.normal(seed, t, x.shape, row_offset) if noise is None else noise[t]) if t > 1 else None
         x = transition(mode, tab, x, t, eps, cond, z)
         if record is not None:
             record.append(x.copy())
@@ -92,18 +94,19 @@ def infer(network, tab, cond, mode="condition_in", noise_condition="sqrt_alpha_b
 
 
 def infer_spectrogram(network, tab, spec, hop_samples, noise_condition="sqrt_alpha_bar", seed=7,
-                      row_offset=0):
-    """SDDM_spectrogram.infer (model/model.py:212-257): x_T = randn(B,1,hop*F)."""
+                      row_offset=0, noise=None):
+    """SDDM_spectrogram.infer (model/model.py:212-257): x_T = randn(B,1,hop*F); noise as infer."""
     T = len(tab["betas"]) - 1
     B = spec.shape[0]
-    x = philox.normal(seed, 0, (B, 1, hop_samples * spec.shape[-1]), row_offset)
+    shape = (B, 1, hop_samples * spec.shape[-1])
+    x = philox.normal(seed, 0, shape, row_offset) if noise is None else noise[0].astype(np.float32)
     for t in range(T, 0, -1):
         if noise_condition == "sqrt_alpha_bar":
             nl = np.full(B, tab["sqrt_alpha_bar"][t], dtype=np.float32)
         else:
             nl = np.full(B, float(t), dtype=np.float32)
         eps = network(spec, x, nl)
-        z = philox.normal(seed, t, x.shape, row_offset) if t > 1 else None
+        z = (philox.normal(seed, t, x.shape, row_offset) if noise is None else noise[t]) if t > 1 else None
         x = transition("original", tab, x, t, eps, None, z)
     return x
 

@@ -237,3 +237,31 @@ def test_torch_cpu_unet_matches_goldens_and_numpy_oracle():
     cond, x, nl = fw[f"fw/{N}/cond"], fw[f"fw/{N}/x_t"], fw[f"fw/{N}/noise_level"]
     ref = ounet.forward(unet_params(N), unet_arch(N), cond, x, nl)
     assert rms(UNetTorch(unet_params(N), unet_arch(N))(cond, x, nl), ref) <= 1e-5
+
+
+# ---------------- the reference's own torch noise (SURVEY §8(b) noise_mode 1) ----------------
+def test_oracle_with_reference_torch_noise():
+    """torch_noise.npz: the reference run with torch.manual_seed(seed) and its own randn draws.
+    model.model.reference_noise re-draws them in the reference's order (CPU generator); the oracle
+    fed with them reproduces the reference output -- pins the draw order the HIP path replays."""
+    import torch
+    import model.diffusion as D
+    import model.model as M
+    import model.network as NW
+    from _helpers import UNET_NET, parse_sched_key, tables_from_golden
+    from oracle import schedule as osched
+    z = golden("torch_noise.npz")
+    for mode in ("condition_in", "supportive"):
+        key = [k.rsplit("/", 1)[0] for k in z.files if k.startswith(f"torchnoise/unet/{mode}/") and k.endswith("/out")][0]
+        sk = key.split("/")[3]
+        N = int(key.split("/")[4].split("x")[0])
+        sched = parse_sched_key(sk)
+        m = M.SDDM(D.GaussianDiffusion(*sched, device="cpu"), NW.UNetModified2(num_samples=N, **UNET_NET["args"]),
+                   p_transition=mode)
+        cond = z[key + "/cond"]
+        torch.manual_seed(int(z[key + "/seed"]))
+        noise = M.reference_noise(m, torch.from_numpy(cond), device="cpu").numpy()
+        P, arch = unet_params(N), unet_arch(N)
+        tab = osched.make_tables(*sched)
+        out = sampler.infer(lambda c, x, nl: unet.forward(P, arch, c, x, nl), tab, cond, mode=mode, noise=noise)
+        assert rms(out, z[key + "/out"]) <= 1e-5, (mode, rms(out, z[key + "/out"]))
