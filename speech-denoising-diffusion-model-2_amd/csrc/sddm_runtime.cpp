@@ -767,7 +767,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   const int team_mode = env_team ? std::atoi(env_team) : c->team;
   const bool team_on = dt != DT_F32 && team_mode != 0 && (env_team != nullptr || PB >= 8);
   const int team_px = env_team_px > 0 ? env_team_px : c->team_px;
-  static const int team_nw = std::getenv("SDDM_TEAM_NW") ? std::atoi(std::getenv("SDDM_TEAM_NW")) : 8;
+  constexpr int team_nw = 8;   // 8-wave team items (the 4-wave variant measured slower)
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
     int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;
@@ -1106,7 +1106,10 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       }
       f.w = WF("final_conv.w");
       f.bias = c->params.at("final_conv.block.3.bias").data[0];
-      f.N = N; f.F = F; f.W = W; f.S = S; f.FT = F % 8 == 0 ? 8 : 2;
+      // frames per block: 8 (512 threads); SDDM_FINAL_FT=16 takes 16 (one 1024-thread block per CU,
+      // 19 staged frame rows per 16 instead of 11 per 8: less halo re-read)
+      static const int env_ft = std::getenv("SDDM_FINAL_FT") ? std::atoi(std::getenv("SDDM_FINAL_FT")) : 0;
+      f.N = N; f.F = F; f.W = W; f.S = S; f.FT = (env_ft == 16 && F % 16 == 0) ? 16 : (F % 8 == 0 ? 8 : 2);
       if (F % f.FT || W % S) FAIL(SDDM_ERR_SHAPE, "final tile: frames %d, segment %d/%d", F, W, S);
       f.co = c->coef();
       const double bytes = (double)B * F * W * src.C * es + (double)B * N * 4 * 3;

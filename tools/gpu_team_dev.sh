@@ -7,5 +7,4 @@ TESTS="tests/test_gpu_unet.py -k team" LOG=team_tests LIMIT=300 bash tools/gpu_t
 TESTS="tests/test_gpu_torch_noise.py tests/test_gpu_long.py" LOG=parity_tests LIMIT=400 bash tools/gpu_tests.sh || exit 1
 SDDM_TEAM=1 SDDM_PLAN_DEBUG=1 bash tools/gpu_team_stamps.sh || exit 1
 cp gpurun_out/team_stamps.log gpurun_out/team_stamps_nw8.log
-SDDM_TEAM=1 SDDM_TEAM_NW=4 bash tools/gpu_team_stamps.sh | head -3 || exit 1
 BENCH=1 bash tools/gpu_ab.sh "SDDM_TEAM=0" "SDDM_TEAM=1" || exit 1

@@ -1,6 +1,6 @@
 """Per-layer timing of one sampling run (HIP events around every launch).
 
-    python tools/profile_ops.py [--batch 16] [--timesteps 20] [--dtype bf16]
+    python tools/profile_ops.py [--batch 16] [--timesteps 20] [--dtype bf16] [--num-samples N] [--lane-rows R]
 """
 import argparse
 import json
@@ -17,6 +17,8 @@ def main():
     ap.add_argument("--timesteps", type=int, default=20)
     ap.add_argument("--dtype", default="bf16")
     ap.add_argument("--json", default=None)
+    ap.add_argument("--num-samples", type=int, default=None, help="chunk length (default: the bench config's)")
+    ap.add_argument("--lane-rows", type=int, default=None, help="rows per lane (bench.py: 64 for batches of 64+)")
     a = ap.parse_args()
     import torch
     from parse_config import ConfigParser, read_json
@@ -27,6 +29,8 @@ def main():
     dev = torch.device("cuda", 0)
     cfg = read_json(os.path.join(REPO, "speech-denoising-diffusion-model-2_amd", "configs", "config_unet_bench.json"))
     cfg["diffusion"]["args"]["n_timestep"] = a.timesteps
+    if a.num_samples:
+        cfg["num_samples"] = a.num_samples
     config = ConfigParser(cfg)
     N = config["num_samples"]
     torch.manual_seed(0)
@@ -34,6 +38,7 @@ def main():
     n = config.init_obj("network", module_network, num_samples=N)
     m = config.init_obj("arch", module_arch, d, n).to(dev)
     m.compute_dtype = {"bf16": "bfloat16", "f16": "float16", "f32": "float32"}[a.dtype]
+    m.lane_rows = a.lane_rows
     cond = torch.from_numpy(noisy_speech(a.batch, N)).to(dev)
     m.infer(cond, seed=1)
     ctx = m._context(dev)

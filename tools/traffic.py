@@ -14,7 +14,11 @@ import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r03_hbm_traffic.json")
+out = sys.argv[1] if len(sys.argv) > 1 else os.path.join(REPO, "profiles", "r04_hbm_traffic.json")
+# workload key (bench.py matches it): N, per-GPU batch, dtype; defaults = the headline config #2
+N_ = int(sys.argv[2]) if len(sys.argv) > 2 else 16448
+B_ = int(sys.argv[3]) if len(sys.argv) > 3 else 16
+DT_ = sys.argv[4] if len(sys.argv) > 4 else "bf16"
 UNET = re.compile(r"conv_in_kernel|conv_strip_kernel|conv_tile_kernel|conv_deep_kernel|final_kernel")
 
 
@@ -46,8 +50,8 @@ for o, f, w in zip(ops, fe, wr):
     k["bytes"] += rd + wb
     k["alg"] += o["bytes"]
 from bench import kernel_src_hash  # noqa: E402
-res = {"N": 16448, "B": 16, "dtype": "bf16", "src": kernel_src_hash(),
-       "what": "HBM bytes per launch of every UNet kernel, one reverse step, B=16 x 16448, bf16",
+res = {"N": N_, "B": B_, "dtype": DT_, "src": kernel_src_hash(),
+       "what": f"HBM bytes per launch of every UNet kernel, one reverse step, B={B_} x {N_}, {DT_}",
        "counters": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) and --pmc WRITE_SIZE, separate passes",
        "step_bytes": round(sum(p["read"] + p["write"] for p in per_op)),
        "step_alg_bytes": round(sum(p["alg_bytes"] for p in per_op)),
