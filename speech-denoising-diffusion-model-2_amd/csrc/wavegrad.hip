@@ -243,23 +243,16 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
   const T* W = (const T*)a.w;
 
   constexpr int PF = PRE == 2 ? PB : 1;
-  // staging unit u -> (row, 16-byte unit q): within each wave-instruction of 64 units the lanes of a
-  // 16-lane group take 64 / UPR consecutive rows at one q, so the group's ds_write_b128 spans land
-  // on distinct 16-byte bank slots of the padded RS-byte rows (rows of 4 whole units per group
-  // collided 2-way); the 64 / UPR rows' units still come from one wave-instruction (coalesced)
-  constexpr int RPB = 64 / UPR;                             // rows per 64-unit block
-  auto urow = [](int u) { return (u >> 6) * RPB + (u & (RPB - 1)); };
-  auto uq = [](int u) { return (u & 63) / RPB; };
   f32x4 breg[PB], areg[PA], shreg[PF], screg[PF];
   const T* film_b = PRE == 2 ? (const T*)a.film + (size_t)b * Tc * 2 * Cin : nullptr;
   auto gload = [&](int c0) {
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int u = tid + j * NT;
-      const int r = urow(u), q = uq(u);
+      const int r = u / UPR, q = u - r * UPR;
       const int tp = t0 - H + r;
       breg[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const bool in = r < rows && tp >= 0 && tp < Tc;
+      const bool in = u < rows * UPR && tp >= 0 && tp < Tc;
       if (in) breg[j] = *(const f32x4*)(src_b + (size_t)wg_map(tp, a.map, a.f) * a.src_C + c0 + q * UE);
       if (PRE == 2 && in) {               // FiLM shift / scale at the conv-input position
         const T* fp = film_b + (size_t)tp * 2 * Cin + c0 + q * UE;
@@ -270,7 +263,7 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const int u = tid + j * NT;
-      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = urow(rem), q = uq(rem);
+      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
       if (u < NAU) areg[j] = *(const f32x4*)(W + ((size_t)(cob + co) * KT + k) * Cin + c0 + q * UE);
     }
   };
@@ -278,8 +271,8 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
 #pragma unroll
     for (int j = 0; j < PB; ++j) {
       const int u = tid + j * NT;
-      const int r = urow(u), q = uq(u);
-      if (r >= rows || u >= NBU) continue;
+      if (u >= rows * UPR) continue;
+      const int r = u / UPR, q = u - r * UPR;
       f32x4 v = breg[j];
       const int tp = t0 - H + r;
       if (PRE == 1) {
@@ -302,7 +295,7 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
     for (int j = 0; j < PA; ++j) {
       const int u = tid + j * NT;
       if (u >= NAU) continue;
-      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = urow(rem), q = uq(rem);
+      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
       *(f32x4*)(wl + (k * WGL_MC + co) * RS + q * 16) = areg[j];
     }
   };
