@@ -160,16 +160,24 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     *(f32x4*)(ring + ((base + r) % R) * SLOT + q * PL + (x + 1) * 16) = v;
   }
 
+  // a 16-pixel column fragment never crosses a row (W % 16 == 0), so its row is wave-uniform: the
+  // per-iteration ring-slot and row arithmetic below is scalar
+  static_assert(W % 32 == 0, "a wave's 32 pixels must not cross rows");
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);
   int prow[FP], pcol[FP];
 #pragma unroll
   for (int fp = 0; fp < FP; ++fp) {
-    const int p = wave * 32 + fp * 16 + (lane & 15);   // pixel inside the MPI-pixel iteration
-    prow[fp] = p / W;
-    pcol[fp] = p % W;
+    // (W % 32 == 0: both fragments of a wave share its row, fragment 1 sits 16 pixels right)
+    prow[fp] = (wave_u * 32) / W;
+    pcol[fp] = (wave_u * 32) % W + fp * 16 + (lane & 15);
   }
   // row-group prefetch geometry of this thread's units (the same every iteration)
   // (all per-iteration address math below is 32-bit with 24-bit multiplies: full-rate VALU)
-  int pr[UPT], uoff[UPT], loff[UPT], cq[UPT];  // row in group, source offset (elements, +A/B flag), LDS offset, channel
+  // (global addresses below are a base plus an unsigned 32-bit byte offset: no sign extensions and,
+  // where the base is uniform, the scalar-base addressing form)
+  int pr[UPT], loff[UPT], cq[UPT];              // row in group, LDS offset, channel
+  const char* rsrc_[UPT];                       // this unit's column / channel in row 0 of its source
+  unsigned rstr[UPT];                           // its source's row stride in bytes
 #pragma unroll
   for (int k = 0; k < UPT; ++k) {
     const int u = tid + k * NT, grp = u >> 6, j = u & 63;
@@ -181,17 +189,16 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     const int c0 = q * VE;
     const int sx = a.upsample ? (x >> 1) : x;
     const bool fa = c0 < a.CA;
-    uoff[k] = (fa ? sx * a.CA + c0 : sx * a.CB + (c0 - a.CA)) * 2 + (fa ? 0 : 1);
+    rsrc_[k] = fa ? (const char*)(srcAb + sx * a.CA + c0) : (const char*)(srcBb + sx * a.CB + (c0 - a.CA));
+    rstr[k] = (unsigned)(a.Wi * (fa ? a.CA : a.CB) * ES);
   }
-  const int rsA = a.Wi * a.CA, rsB = a.Wi * a.CB;          // elements per source row
   // rows of row group j (clamped: the groups past the strip end load valid rows nobody reads)
   auto issue_rows = [&](f32x4 (&dst)[UPT], int j) {
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
       const int ry = min(y0 + j * TR + 1 + pr[k], H - 1);
       const int sy = a.upsample ? (ry >> 1) : ry;
-      const bool fb = uoff[k] & 1;
-      dst[k] = *(const f32x4*)((fb ? srcBb : srcAb) + ((uoff[k] >> 1) + (int)__umul24(sy, fb ? rsB : rsA)));
+      dst[k] = *(const f32x4*)(rsrc_[k] + (unsigned)__umul24((unsigned)sy, rstr[k]));
     }
   };
   // ring slots of row group j (group iters, past the strip, lands in slots nobody reads again)
@@ -219,9 +226,9 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp) {
       const int yy = min(y0 + it * TR, H - TR) + prow[fp];
-      const int po = (int)__umul24(yy * W + pcol[fp], a.Cout);
+      const unsigned po = (unsigned)(yy * W * a.Cout) + __umul24((unsigned)pcol[fp], (unsigned)a.Cout) + n0 + 4 * g;
 #pragma unroll
-      for (int fc = 0; fc < FC; ++fc) dst[fp][fc] = *(const vec4*)(resb + (po + n0 + fc * 16 + 4 * g));
+      for (int fc = 0; fc < FC; ++fc) dst[fp][fc] = *(const vec4*)((const char*)resb + (po * ES + fc * 16 * ES));
     }
   };
   const T* rawAb = RES == 2 ? (const T*)a.rawA + (size_t)b * H * W * a.RCA : outb;
@@ -284,7 +291,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       for (int dy = 0; dy < 3; ++dy) {
         int sl = s_it + prow[fp] + dy;                   // < 2R: one conditional wrap
         sl = sl >= R ? sl - R : sl;
-        bptr[fp][dy] = ring + (int)__umul24(sl, SLOT) + g * UPL * PL + pcol[fp] * 16;
+        bptr[fp][dy] = ring + (sl * SLOT + (g * UPL * PL + pcol[fp] * 16));
       }
     // the ring refill of row group it + 1 (its rows were issued an iteration ago) is transformed
     // between the taps' MFMAs, unit k after tap k * 9 NCK / UPT, and stored after the epilogue
@@ -323,17 +330,17 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     // ---- epilogue: bias + embedding + residual, store, statistics ----
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp) {
-      const int po = (int)__umul24((y + prow[fp]) * W + pcol[fp], a.Cout);
+      const unsigned po = (unsigned)((y + prow[fp]) * W * a.Cout) + __umul24((unsigned)pcol[fp], (unsigned)a.Cout);
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) {
-        const int co = n0 + fc * 16 + 4 * g;
+        const unsigned co = n0 + fc * 16 + 4 * g;
         // statistics of the fp32 values (before the storage rounding), about the shift badd
         f32x2 d0 = f32x2{acc[fp][fc][0], acc[fp][fc][1]}, d1 = f32x2{acc[fp][fc][2], acc[fp][fc][3]};
         if constexpr (RES == 1) {
           d0 += unpack2<T>(r1cur[fp][fc][0], r1cur[fp][fc][1]);
           d1 += unpack2<T>(r1cur[fp][fc][2], r1cur[fp][fc][3]);
         }
-        store4p<T>(outb + (po + co), d0 + bp[fc][0], d1 + bp[fc][1]);
+        store4p<T>((T*)((char*)outb + (po + co) * ES), d0 + bp[fc][0], d1 + bp[fc][1]);
         s1[fc][0] += d0;
         s1[fc][1] += d1;
         s2[fc][0] = __builtin_elementwise_fma(d0, d0, s2[fc][0]);
