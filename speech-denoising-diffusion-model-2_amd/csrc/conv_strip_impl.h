@@ -32,6 +32,12 @@
 #pragma once
 #include <type_traits>
 
+// timing-ablation builds only (tools/gpu_ablate.sh): 16 every tap reads the same weight fragment,
+// 256 every tap reads the same input fragment (results are garbage)
+#ifndef SDDM_ABL_STRIP
+#define SDDM_ABL_STRIP 0
+#endif
+
 #include "conv_common.h"
 #include "kernels.h"
 
@@ -273,8 +279,15 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
                   vec4 (&r1nxt)[FP][FC], Frag<T> (&r2cur)[RCKM][FP], Frag<T> (&r2nxt)[RCKM][FP]) {
     const int y = y0 + it * TR;
     const int s_it = (base + it * TR) % R;               // slot of row y - 1
-    if constexpr (decltype(LR)::value) issue_rows(nxt, it + 2);
-    if constexpr (RES == 1 && decltype(LX)::value) issue_res1(r1nxt, it + 1);
+#ifdef SDDM_STAMPS
+    // timing ablations of the profiling build (SDDM_STAMPS_DBG): 4 no row loads, 64 no residual
+    // loads, 8 no MFMAs, 2 no staging transform, 128 no output stores (results are garbage)
+    const int dbg = a.dbg;
+#else
+    constexpr int dbg = 0;
+#endif
+    if constexpr (decltype(LR)::value) if (!(dbg & 4)) issue_rows(nxt, it + 2);
+    if constexpr (RES == 1 && decltype(LX)::value) if (!(dbg & 64)) issue_res1(r1nxt, it + 1);
     if constexpr (RES == 2 && decltype(LX)::value) issue_res2(r2nxt, it + 1);
     // keep these loads at the top of the body: the scheduler would otherwise sink them below the
     // MFMAs (shorter live ranges) and halve the prefetch distance
@@ -303,16 +316,18 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         const int dy = tap / 3, dx = tap - 3 * dy;
         Frag<T> bf[FP];
 #pragma unroll
-        for (int fp = 0; fp < FP; ++fp) bf[fp] = load_planes<T>(bptr[fp][dy] + ck * 4 * UPL * PL + dx * 16, PL);
+        for (int fp = 0; fp < FP; ++fp)   // (SDDM_ABL_STRIP & 256: every tap reads tap 0's fragment)
+          bf[fp] = load_planes<T>((SDDM_ABL_STRIP & 256) ? bptr[fp][0] : bptr[fp][dy] + ck * 4 * UPL * PL + dx * 16, PL);
 #pragma unroll
         for (int fc = 0; fc < FC; ++fc) {
-          const Frag<T> af = load_planes<T>(abase + (ck * 9 + tap) * 4 * UPL * WPL + fc * 256, WPL);
+          const Frag<T> af = load_planes<T>(abase + ((SDDM_ABL_STRIP & 16) ? 0 : (ck * 9 + tap) * 4 * UPL * WPL) + fc * 256, WPL);
 #pragma unroll
-          for (int fp = 0; fp < FP; ++fp) mfma_frag(acc[fp][fc], af, bf[fp]);
+          for (int fp = 0; fp < FP; ++fp)
+            if (!(dbg & 8)) mfma_frag(acc[fp][fc], af, bf[fp]);
         }
 #pragma unroll
         for (int k = 0; k < UPT; ++k)                      // (the last iteration refills nothing)
-          if (decltype(LX)::value && ck * 9 + tap == k * 9 * NCK / UPT) tv[k] = xform_unit(fill, it + 1, k);
+          if (decltype(LX)::value && ck * 9 + tap == k * 9 * NCK / UPT) tv[k] = (dbg & 2) ? fill[k] : xform_unit(fill, it + 1, k);
       }
     }
     if constexpr (RES == 2) {  // ResnetBlock.res_conv 1x1 on the raw block input (fragments prefetched)
@@ -340,7 +355,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
           d0 += unpack2<T>(r1cur[fp][fc][0], r1cur[fp][fc][1]);
           d1 += unpack2<T>(r1cur[fp][fc][2], r1cur[fp][fc][3]);
         }
-        store4p<T>((T*)((char*)outb + (po + co) * ES), d0 + bp[fc][0], d1 + bp[fc][1]);
+        if (!(dbg & 128)) store4p<T>((T*)((char*)outb + (po + co) * ES), d0 + bp[fc][0], d1 + bp[fc][1]);
         s1[fc][0] += d0;
         s1[fc][1] += d1;
         s2[fc][0] = __builtin_elementwise_fma(d0, d0, s2[fc][0]);

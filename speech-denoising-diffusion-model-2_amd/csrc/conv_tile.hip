@@ -255,14 +255,21 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   transform(0, 0);
   dma_sync();                                              // operand image 0, weights 0 (LDS-DMA)
   SDDM_STAMP(a, 2);
+#ifdef SDDM_STAMPS
+  // timing ablations of the profiling build (SDDM_STAMPS_DBG): 4 no raw loads, 32 no weight DMA,
+  // 8 no MFMAs, 2 no staging transform, 128 no output stores (results are garbage)
+  const int dbg = a.dbg;
+#else
+  constexpr int dbg = 0;
+#endif
   for (int k = 0; k < nk; ++k) {
     const int cur = k & 1, nxt = cur ^ 1;
     if (k + 1 < nk) {
-      load_raw(k + 1);                                     // in flight during the MFMAs
-      issue_w(k + 1, nxt);                                 // WB[nxt] was read by chunk k - 1
+      if (!(dbg & 4)) load_raw(k + 1);                     // in flight during the MFMAs
+      if (!(dbg & 32)) issue_w(k + 1, nxt);                // WB[nxt] was read by chunk k - 1
     }
-    mma(k, cur);
-    if (k + 1 < nk) transform(k + 1, nxt);                 // IB[nxt] was read by chunk k - 1
+    if (!(dbg & 8)) mma(k, cur);
+    if (k + 1 < nk && !(dbg & 2)) transform(k + 1, nxt);   // IB[nxt] was read by chunk k - 1
     dma_sync();                                            // WB[nxt] landed by LDS-DMA from every wave
   }
   SDDM_STAMP(a, 4);
@@ -285,7 +292,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
       float d[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) d[i] = acc[fp][fc][i] + (ident ? to_f32<T>(r1[fp][fc][i]) : 0.f);
-      store4<T>(out + po + co, d[0] + bb[fc][0], d[1] + bb[fc][1], d[2] + bb[fc][2], d[3] + bb[fc][3]);
+      if (!(dbg & 128)) store4<T>(out + po + co, d[0] + bb[fc][0], d[1] + bb[fc][1], d[2] + bb[fc][2], d[3] + bb[fc][3]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {                        // sums about the shift bb (stable)
         s1[fc][i] += d[i];

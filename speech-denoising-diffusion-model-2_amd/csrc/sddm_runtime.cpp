@@ -979,6 +979,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
           SDDM_HIP_CHECK(hipMemset(c->stamp_buf, 0, sizeof(unsigned long long) * 8 * 65536));
           a.stamps = c->stamp_buf;
+          if (const char* f = std::getenv("SDDM_STAMPS_DBG")) a.dbg = std::atoi(f);   // timing ablations
           int nb = 32;
           if (ch.tile >= 0) { const TileCfg tc = conv_tile_cfg(ch.tile); nb = tc.wco * tc.fc * 16; }
           c->stamp_blocks = ch.strip ? (int64_t)(a.Ho / ch.SR) * B * ((a.Cout + ch.nblk - 1) / ch.nblk)
