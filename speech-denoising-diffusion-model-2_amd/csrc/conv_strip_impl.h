@@ -37,6 +37,9 @@
 #ifndef SDDM_ABL_STRIP
 #define SDDM_ABL_STRIP 0
 #endif
+#ifndef SDDM_STRIP_WREG
+#define SDDM_STRIP_WREG 1   // 0: weight fragments re-read from LDS every iteration (A/B builds)
+#endif
 
 #include "conv_common.h"
 #include "kernels.h"
@@ -275,6 +278,11 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   // it + 1 and refill the ring; the last two iterations of a strip issue no rows and the last
   // neither residual inputs nor a refill (the groups past the strip end were once loaded clamped
   // and never read: up to 2x the input bytes of the 2-iteration level-1 strips)
+  // one input-channel chunk, two channel fragments, 16-bit storage, no res_conv: the 9 x FC weight
+  // fragments stay in VGPRs for the whole strip (72 VGPRs) instead of being re-read from LDS by
+  // every iteration (half the operand reads)
+  constexpr bool WREG = SDDM_STRIP_WREG && ES == 2 && NCK == 1 && FC == 2 && RES != 2 && MPI == 256;
+  Frag<T> wreg[WREG ? 9 : 1][FC];
   auto body = [&](auto LR, auto LX, int it, f32x4 (&nxt)[UPT], f32x4 (&fill)[UPT], vec4 (&r1cur)[FP][FC],
                   vec4 (&r1nxt)[FP][FC], Frag<T> (&r2cur)[RCKM][FP], Frag<T> (&r2nxt)[RCKM][FP]) {
     const int y = y0 + it * TR;
@@ -320,7 +328,8 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
           bf[fp] = load_planes<T>((SDDM_ABL_STRIP & 256) ? bptr[fp][0] : bptr[fp][dy] + ck * 4 * UPL * PL + dx * 16, PL);
 #pragma unroll
         for (int fc = 0; fc < FC; ++fc) {
-          const Frag<T> af = load_planes<T>(abase + ((SDDM_ABL_STRIP & 16) ? 0 : (ck * 9 + tap) * 4 * UPL * WPL) + fc * 256, WPL);
+          const Frag<T> af = WREG ? wreg[WREG ? tap : 0][fc]
+                                  : load_planes<T>(abase + ((SDDM_ABL_STRIP & 16) ? 0 : (ck * 9 + tap) * 4 * UPL * WPL) + fc * 256, WPL);
 #pragma unroll
           for (int fp = 0; fp < FP; ++fp)
             if (!(dbg & 8)) mfma_frag(acc[fp][fc], af, bf[fp]);
@@ -373,6 +382,12 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   constexpr int NYOUNG = UPT + (RES == 1 ? FP * FC : 0) + (RES == 2 ? RCKM * FP : 0);
   static_assert(NYOUNG < 64, "vmcnt is a 6-bit counter");
   asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" :: "n"(NYOUNG) : "memory");
+  if constexpr (WREG) {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) wreg[tap][fc] = load_planes<T>(abase + tap * 4 * UPL * WPL + fc * 256, WPL);
+  }
   SDDM_STAMP(a, 3);
   using yes = std::integral_constant<bool, true>;
   using no = std::integral_constant<bool, false>;
