@@ -139,7 +139,10 @@ def kernel_src_hash():
     import glob
     import hashlib
     h = hashlib.sha256()
-    files = sorted(glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h")))
+    # (the spectrogram samplers' sources are left out: they run none of the UNet's kernels)
+    other = {"diffwave.hip", "dw_runtime.h", "wavegrad.hip", "wg_kernels.h", "wg_runtime.h", "stft.hip", "stft_kernels.h"}
+    files = sorted(f for f in glob.glob(os.path.join(PKG, "csrc", "*.hip")) + glob.glob(os.path.join(PKG, "csrc", "*.h"))
+                   if os.path.basename(f) not in other)
     files += [os.path.join(PKG, "csrc", "sddm_runtime.cpp"), os.path.join(PKG, "configs", "conv_tuning.json")]
     for f in files:
         with open(f, "rb") as fh:
