@@ -578,7 +578,7 @@ static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   }
   if (a.TR * a.TW > MT || a.Cout % NB || (a.CA + a.CB) % 32 || (a.CA + a.CB) > 1000 || (a.RCA + a.RCB) % 32)
     return hipErrorInvalidValue;
-  if (lay.total > 160 * 1024) return hipErrorInvalidValue;
+  if (lay.total > kLdsBytes) return hipErrorInvalidValue;
   const dim3 grid = xcd_grid(a.n_tiles, B, a.Cout / NB), blk(64 * NW);
   const int D = deep_ring<T, MT, NW>((nck * 9 + rck + NW - 1) / NW);
 #define SDDM_RING(DV)                                                                         \

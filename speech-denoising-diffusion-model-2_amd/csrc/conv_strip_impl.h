@@ -445,7 +445,7 @@ static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size
   const size_t lds = strip_lds<T, FC, W, CIN, MPI>(a);
   if (lo) { *lo = lds; return hipSuccess; }
   constexpr int TR = MPI / W;
-  if (lds > 160 * 1024 || a.Ho % SR || SR % (2 * TR) || a.Cout % (16 * FC) || a.res_mode < 0 || a.res_mode > 2 ||
+  if (lds > kLdsBytes || a.Ho % SR || SR % (2 * TR) || a.Cout % (16 * FC) || a.res_mode < 0 || a.res_mode > 2 ||
       (a.res_mode == 2 && (a.RCA + a.RCB) > 128))
     return hipErrorInvalidValue;
   if (a.n_tiles != a.Ho / SR) return hipErrorInvalidValue;

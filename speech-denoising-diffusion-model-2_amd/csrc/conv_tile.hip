@@ -352,7 +352,7 @@ static hipError_t tile_go(const ConvArgs& a, int B, hipStream_t s) {
   constexpr int MT = c.wpx * c.fp * 16, NB = c.wco * c.fc * 16;
   const size_t lds = tile_lds_cfg<I>(S2, a);
   if (a.TR * a.TW > MT || a.Cout % NB || (a.CA + a.CB) % 32 || a.CA % 32 || (a.RCA + a.RCB) % 32 || a.RCA % 32 ||
-      lds > 160 * 1024 || !a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))
+      lds > kLdsBytes || !a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))
     return hipErrorInvalidValue;
   hipLaunchKernelGGL((conv_tile_kernel<T, S2, c.wpx, c.wco, c.fp, c.fc, S2 ? c.maxu_s2 : c.maxu>),
                      xcd_grid(a.n_tiles, B, a.Cout / NB), dim3(64 * c.wpx * c.wco), lds, s, a);

@@ -124,7 +124,10 @@ struct TeamArgs {
                               //  staged, K loop done, stored, statistics written}
 };
 // nw = 4: two 4-wave workgroups per CU (64 per XCD); nw = 8: one 8-wave workgroup per CU (32 per XCD)
-constexpr int team_lds_budget(int nw) { return nw == 8 ? 160 * 1024 : 80 * 1024; }
+// LDS per workgroup every launcher and planner sizes against: gfx950's 160 KiB (sddm_create fails
+// on a device that offers less, so no plan is built for LDS the device does not have)
+constexpr int kLdsBytes = 160 * 1024;
+constexpr int team_lds_budget(int nw) { return nw == 8 ? kLdsBytes : kLdsBytes / 2; }
 constexpr int kTeamSlot = 64;                 // words per team counter (256 bytes)
 hipError_t launch_conv_team(int dtype, int nw, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s);
 int conv_team_var(bool s2, int mt, int nb);  // -1: no team variant for this tiling

@@ -557,7 +557,7 @@ hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
   // the whole grid resident in one round); one pass of 4 samples per thread covers a block's
   // samples (the last block's tail included)
   const int nt = a.FT >= 16 ? 1024 : 512;
-  if (lds > 160 * 1024 || a.F % a.FT || a.C != 32 || a.FT * a.S + a.W > 4 * nt || a.N % 4) return hipErrorInvalidValue;
+  if (lds > kLdsBytes || a.F % a.FT || a.C != 32 || a.FT * a.S + a.W > 4 * nt || a.N % 4) return hipErrorInvalidValue;
   dim3 grid(a.F / a.FT, B);
 #define SDDM_FINAL(TT)                                                                    \
   if (nt == 1024) hipLaunchKernelGGL((final_kernel<TT, 1024>), grid, dim3(1024), lds, s, a); \

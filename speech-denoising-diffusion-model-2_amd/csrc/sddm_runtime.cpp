@@ -538,7 +538,7 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
     a.TR = TR; a.TW = TW; a.tiles_x = a.Wo / TW; a.n_tiles = a.tiles_x * (a.Ho / TR);
     for (int nw : {8, 4}) {
       a.deep_nw = nw;
-      if (conv_deep_lds_bytes(dt, mt, s2, a) > 160 * 1024) continue;
+      if (conv_deep_lds_bytes(dt, mt, s2, a) > kLdsBytes) continue;
       const int blocks = a.n_tiles * B * nz, per_round = 256 * (nw == 4 ? 2 : 1);
       cs.push_back({mt, nw, TR, TW, a.tiles_x, a.n_tiles, blocks, (blocks + per_round - 1) / per_round});
     }
@@ -634,7 +634,7 @@ static bool choose_tile(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
     if (a.Ho % TR) continue;
     if (TR * TW < MT && (TR != a.Ho || TW != a.Wo)) continue;   // partial tiles: whole small images only
     a.TR = TR; a.TW = TW; a.tiles_x = a.Wo / TW; a.n_tiles = a.tiles_x * (a.Ho / TR);
-    if (conv_tile_lds_bytes(cfg, s2, a) > 160 * 1024) continue;
+    if (conv_tile_lds_bytes(cfg, s2, a) > kLdsBytes) continue;
     cs.push_back({cfg, TR, TW, a.tiles_x, a.n_tiles, a.n_tiles * B * (a.Cout / NB), TR * TW * NB});
   }
   if (cs.empty()) return false;
@@ -676,7 +676,7 @@ static bool choose_conv(int dt, int B, int Cin, int RC, int res_mode, int Ho, in
       if (Ho % TRs) continue;
       for (int ni = 0; ni < 2; ++ni) {
         const int nb = nbs[ni];
-        if (conv_strip_lds_bytes(dt, nb, mpi, a) > 160 * 1024) continue;
+        if (conv_strip_lds_bytes(dt, nb, mpi, a) > kLdsBytes) continue;
         const int nz = (Cout + nb - 1) / nb;
         int SR = 0;
         const int target = env_blocks ? env_blocks : 256;
@@ -1248,6 +1248,10 @@ int sddm_create(int device, int compute_dtype, sddm_ctx** out) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
     FAIL(SDDM_ERR_HIP, "no HIP device %d (count %d)", device, n);
+  int lds = 0;
+  if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess || lds < kLdsBytes)
+    FAIL(SDDM_ERR_HIP, "device %d offers %d bytes of LDS per workgroup; the kernels are planned for %d (gfx950)", device,
+         lds, kLdsBytes);
   sddm_ctx* c = new sddm_ctx();
   c->device = device;
   c->dtype = compute_dtype;
