@@ -230,9 +230,19 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
   constexpr int SROWS = WGL_MT + 2 * WGL_HALO;
   constexpr int NBU = SROWS * UPR, NAU = KT * WGL_MC * UPR;
   constexpr int PB = (NBU + NT - 1) / NT, PA = (NAU + NT - 1) / NT;
-  __shared__ __attribute__((aligned(16))) char lds[(SROWS + KT * WGL_MC) * RS];
+  // 16-bit storage: plane-major images (a plane = one 16-byte channel unit of every row, plane
+  // stride 0 mod 256 B) with the row slot XOR-swizzled by 2 x plane, so the staging stores (8-lane
+  // groups: 2 rows x 4 planes) and the MFMA operand reads (ds_read_b128 lane groups mixing 8 rows
+  // of two planes) hit distinct banks; fp32 keeps the padded row-major image
+  constexpr bool SW = ES == 2;
+  constexpr int PSB = (SROWS * 16 + 255) / 256 * 256, PSW = (KT * WGL_MC * 16 + 255) / 256 * 256;
+  constexpr int SLAB_BYTES = SW ? UPR * PSB : SROWS * RS, WL_BYTES = SW ? UPR * PSW : KT * WGL_MC * RS;
+  static_assert(!SW || (SROWS % 8 == 0 && UPR <= 4), "the swizzle stays inside aligned 8-row groups");
+  __shared__ __attribute__((aligned(16))) char lds[SLAB_BYTES + WL_BYTES];
   char* slab = lds;
-  char* wl = lds + SROWS * RS;
+  char* wl = lds + SLAB_BYTES;
+  auto sadr = [](int r, int q) { return SW ? q * PSB + ((r ^ (q << 1)) << 4) : r * RS + q * 16; };
+  auto wadr = [](int r, int q) { return SW ? q * PSW + ((r ^ (q << 1)) << 4) : r * RS + q * 16; };
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, l16 = lane & 15;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -289,14 +299,14 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
         for (int e = 0; e < UE; ++e) x[e] = from_f32<T>(wg_leaky(to_f32<T>(sh[e]) + to_f32<T>(sc[e]) * to_f32<T>(x[e])));
         v = __builtin_bit_cast(f32x4, x);
       }
-      *(f32x4*)(slab + r * RS + q * 16) = v;
+      *(f32x4*)(slab + sadr(r, q)) = v;
     }
 #pragma unroll
     for (int j = 0; j < PA; ++j) {
       const int u = tid + j * NT;
       if (u >= NAU) continue;
       const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
-      *(f32x4*)(wl + (k * WGL_MC + co) * RS + q * 16) = areg[j];
+      *(f32x4*)(wl + wadr(k * WGL_MC + co, q)) = areg[j];
     }
   };
 
@@ -306,6 +316,7 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
 #pragma unroll
     for (int p = 0; p < 4; ++p) acc[i][p] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int wc = (wave & 1) * 64, wt = (wave >> 1) * 64;
+  const int wa0 = SW ? wadr(wc + l16, g) : 0;
   const int ncs = Cin / 32;
   gload(0);
   for (int cc = 0; cc < ncs; ++cc) {
@@ -317,9 +328,12 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
     for (int k = 0; k < KT; ++k) {
       Frag<T> af[4], bf[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = load_frag<T>(wl + (k * WGL_MC + wc + i * 16 + l16) * RS + g * 8 * ES);
+      for (int i = 0; i < 4; ++i)   // (rows k * 128 + i * 16 keep the swizzled low bits: constant offsets)
+        af[i] = load_frag<T>(wl + (SW ? wa0 + (k * WGL_MC + i * 16) * 16 : (k * WGL_MC + wc + i * 16 + l16) * RS + g * 8 * ES));
+      const int sbk = SW ? sadr(wt + l16 + k * a.dil, g) : 0;
 #pragma unroll
-      for (int p = 0; p < 4; ++p) bf[p] = load_frag<T>(slab + (wt + p * 16 + l16 + k * a.dil) * RS + g * 8 * ES);
+      for (int p = 0; p < 4; ++p)
+        bf[p] = load_frag<T>(slab + (SW ? sbk + p * 16 * 16 : (wt + p * 16 + l16 + k * a.dil) * RS + g * 8 * ES));
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
