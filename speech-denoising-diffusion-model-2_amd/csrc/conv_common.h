@@ -212,12 +212,19 @@ namespace sddm {
 #define SDDM_STAMP(args, k) do {} while (0)
 #endif
 
+#ifndef SDDM_XCD_ZIN
+#define SDDM_XCD_ZIN 1   // strip and K-streamed tile blocks: channel block innermost (0: z-major, A/B builds)
+#endif
+
 // XCD-aware block order.  The logical grid (X tiles, Y images, Z channel blocks) is launched as
 // one dimension; blocks are dealt round-robin over the 8 XCDs (block id % 8 shares an L2), so
 // block id is mapped to position (id % 8) * total/8 + id / 8 of the z-major order: each XCD's
 // blocks cover one contiguous run of channel blocks (the same weight slices) and of images and
 // adjacent tiles (shared halos) and read them from its own L2 instead of each XCD fetching every
 // weight slice.  Speed only, never correctness (HIP does not promise the placement).
+// ZIN (channel block innermost): the channel blocks of one tile share an XCD, so the second
+// block's input reads hit that XCD's L2 (layers whose weights are small next to their inputs)
+template <bool ZIN = false>
 __device__ __forceinline__ void xcd_block(int X, int Z, int& x, int& y, int& z) {
   if (gridDim.y > 1 || gridDim.z > 1) {             // launched in plain (x, y, z) order
     x = blockIdx.x; y = blockIdx.y; z = blockIdx.z;
@@ -226,6 +233,13 @@ __device__ __forceinline__ void xcd_block(int X, int Z, int& x, int& y, int& z) 
   const int total = (int)gridDim.x, Y = total / (X * Z);
   const int id = (int)blockIdx.x;
   const int j = (total & 7) == 0 ? (id & 7) * (total >> 3) + (id >> 3) : id;
+  if (ZIN) {
+    z = j % Z;
+    const int r = j / Z;
+    x = r % X;
+    y = r / X;
+    return;
+  }
   x = j % X;
   const int r = j / X;
   y = r % Y;

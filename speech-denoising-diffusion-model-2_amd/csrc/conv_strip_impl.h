@@ -73,7 +73,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   int strip, b, zb;
-  xcd_block(a.n_tiles, a.Cout / NBLK, strip, b, zb);
+  xcd_block<SDDM_XCD_ZIN != 0>(a.n_tiles, a.Cout / NBLK, strip, b, zb);
   const int n0 = zb * NBLK;
   const int H = a.Ho;
   const int RC = a.RCA + a.RCB;

@@ -45,7 +45,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wp = wv % WPX, wc = wv / WPX;
   int tile, b, zb;
-  xcd_block(a.n_tiles, a.Cout / NB, tile, b, zb);
+  xcd_block<SDDM_XCD_ZIN != 0>(a.n_tiles, a.Cout / NB, tile, b, zb);
   const int n0 = zb * NB;
   const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
   const int y0 = ty * a.TR, x0 = tx * a.TW;
