@@ -141,22 +141,7 @@ struct GNFuse {
   int G; float eps;
 };
 
-// Loads of bytes another workgroup of the same launch stored (HO, conv_deep.hip's team kernel):
-// buffer loads with sc1 over a resource based at the lane arena `hb` (every activation and
-// statistics tensor lies in it, < 4 GiB), served by the XCD's L2 past this CU's L1.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t ho_rsrc(const char* hb) {
-  return __builtin_amdgcn_make_buffer_rsrc((void*)hb, (short)0, -1, 0x00020000);
-}
-template <bool HO = false>
-__device__ __forceinline__ float ld_stat(const float* p, const char* hb) {
-  if constexpr (HO)
-    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(ho_rsrc(hb), (unsigned)((const char*)p - hb), 0, 16));
-  else return *p;
-}
-
-template <bool HO = false>
-__device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh,
-                                                  const char* hb = nullptr) {
+__device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
   const int C = CA + CB, cpg = C / f.G;
   const int tpg = pow2_floor(blockDim.x / f.G);   // threads per group (power of two, <= 64)
   const int g = threadIdx.x / tpg, sub = threadIdx.x - g * tpg;
@@ -173,7 +158,7 @@ __device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA
   double s = 0.0;
   for (int i = sub; i < items; i += tpg) {
     const int c = i / tiles, t = i - c * tiles;
-    s += (double)ld_stat<HO>(base + ((size_t)t * Cs + cs0 + c) * 2, hb);
+    s += (double)base[((size_t)t * Cs + cs0 + c) * 2];
   }
   for (int o = 1; o < tpg; o <<= 1) s += __shfl_xor(s, o);
   const double n_tot = (double)items * ntile;
@@ -182,8 +167,8 @@ __device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA
   for (int i = sub; i < items; i += tpg) {
     const int c = i / tiles, t = i - c * tiles;
     const float* e = base + ((size_t)t * Cs + cs0 + c) * 2;
-    const double d = (double)ld_stat<HO>(e, hb) / ntile - mean;
-    m2 += (double)ld_stat<HO>(e + 1, hb) + (double)ntile * d * d;
+    const double d = (double)e[0] / ntile - mean;
+    m2 += (double)e[1] + (double)ntile * d * d;
   }
   for (int o = 1; o < tpg; o <<= 1) m2 += __shfl_xor(m2, o);
   const double rstd = 1.0 / sqrt(m2 / n_tot + (double)f.eps);
@@ -197,19 +182,20 @@ __device__ __forceinline__ void gn_fused_prologue(const GNFuse& f, int b, int CA
 }  // namespace sddm
 
 namespace sddm {
-// Phase timestamps (profiling builds with -DSDDM_STAMPS only): slot 0 / 7 = s_memrealtime (100 MHz)
-// at block start / end, slots 1..6 = s_memtime (shader clock) at the kernel's phase boundaries.
+// Phase timestamps (profiling builds with -DSDDM_STAMPS only): s_memrealtime (100 MHz) of wave 0
+// at block start (slot 0), at the kernel's phase boundaries (slots 1..6) and at block end (slot 7).
+// The flat block index comes from the kernel (blockIdx only): gridDim would be read from the
+// implicit kernel arguments by a vector load whose wait drains every load in flight.
 #ifdef SDDM_STAMPS
-#define SDDM_STAMP(args, k)                                                                       \
+#define SDDM_STAMP(args, k) SDDM_STAMP_AT(args, k, blockIdx.x)
+#define SDDM_STAMP_AT(args, k, blk)                                                               \
   do {                                                                                            \
-    if ((args).stamps && threadIdx.x == 0) {                                                      \
-      const size_t blk_ = blockIdx.x + (size_t)gridDim.x * (blockIdx.y + (size_t)gridDim.y * blockIdx.z); \
-      (args).stamps[blk_ * 8 + (k)] = ((k) == 0 || (k) == 7) ? __builtin_amdgcn_s_memrealtime()    \
-                                                             : __builtin_amdgcn_s_memtime();      \
-    }                                                                                             \
+    if ((args).stamps && threadIdx.x == 0)                                                        \
+      (args).stamps[(size_t)(blk) * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                  \
   } while (0)
 #else
 #define SDDM_STAMP(args, k) do {} while (0)
+#define SDDM_STAMP_AT(args, k, blk) do {} while (0)
 #endif
 
 #ifndef SDDM_XCD_ZIN
@@ -259,8 +245,9 @@ __device__ __forceinline__ int fdivi(int n, float rd) { return (int)(((float)n +
 // GroupNorm statistics of one group loaded in a single round trip (issue() before anything waits,
 // finish() after): up to GK (sum, M2) items per thread; larger producers fall back to the
 // two-pass loop of gn_fused_prologue (fp64).  Chan combination in a fixed order.
-struct GNLoad {
-  static constexpr int GK = 12;
+template <int GK_ = 12>
+struct GNLoadT {
+  static constexpr int GK = GK_;
   float2 v[GK];
   float gm, bt;                 // gamma / beta of channel c0 + sub (sub < cpg), loaded with the items
   int items, tpg, sub, grp, ntile;
@@ -270,9 +257,7 @@ struct GNLoad {
   // readable address): the kernels call issue() unconditionally, because a load inside a branch
   // makes the compiler wait for it at the branch join, serialising this round trip in front of
   // every other load of the prologue.
-  template <bool HO = false>
-  __device__ __forceinline__ void issue(const GNFuse& f, int b, int CA, int CB, bool on, const float* safe,
-                                        const char* hb = nullptr) {
+  __device__ __forceinline__ void issue(const GNFuse& f, int b, int CA, int CB, bool on, const float* safe) {
     const int G = f.G > 0 ? f.G : 32;
     const int C = CA + CB, cpg = C / G;
     tpg = pow2_floor(blockDim.x / G);                 // xor butterflies: a power of two (6-wave blocks)
@@ -297,23 +282,16 @@ struct GNLoad {
       const int i = min(sub + k * tpg, items - 1);
       const int c = fdivi(i, rt), t = i - c * tiles;
       const int off = on ? (t * Cs + cs0 + c) * 2 : 0;   // 32-bit offsets: no 64-bit address math
-      if constexpr (HO) {
-        const unsigned long long u = __builtin_bit_cast(unsigned long long, __builtin_amdgcn_raw_buffer_load_b64(
-            ho_rsrc(hb), (unsigned)((const char*)(base + off) - hb), 0, 16));
-        v[k] = make_float2(__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32)));
-      }
-      else v[k] = *(const float2*)(base + off);
+      v[k] = *(const float2*)(base + off);
     }
     const int cg = on ? c0 + min(sub, cpg - 1) : 0;   // clamped: unconditional loads
     gm = (on ? f.gamma : safe)[cg];
     bt = (on ? f.beta : safe)[cg];
   }
 
-  template <bool HO = false>
-  __device__ __forceinline__ void finish(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh,
-                                         const char* hb = nullptr) {
+  __device__ __forceinline__ void finish(const GNFuse& f, int b, int CA, int CB, float* sc, float* sh) {
     if (!fast) {
-      gn_fused_prologue<HO>(f, b, CA, CB, sc, sh, hb);
+      gn_fused_prologue(f, b, CA, CB, sc, sh);
       return;
     }
     if (grp >= f.G) return;
@@ -351,6 +329,7 @@ struct GNLoad {
     }
   }
 };
+using GNLoad = GNLoadT<12>;
 
 // =============================================================================================
 // Per-channel tile statistics from an fp32 LDS tile [npix][ld] (values already rounded to the

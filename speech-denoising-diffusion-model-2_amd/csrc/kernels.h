@@ -42,8 +42,6 @@ struct ConvInArgs {
   float* stats;               // [B][tiles][Cout][2]
   int TR;                     // frame rows per block
   int* t_dev;                 // step counter decremented once per launch (may be null)
-  unsigned* zero; int nzero;  // words zero[i * kTeamSlot], i < nzero, cleared by the launch (team-kernel
-                              // counters of the step; may be null)
   unsigned long long* stamps; // SDDM_STAMPS builds only
 };
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s);
@@ -101,36 +99,9 @@ hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a);
 int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps);   // the D template argument (profiles)
 
-// ---- deep-level team kernel (conv_deep.hip): a run of consecutive convolutions as one launch,
-// image b served by the workgroups of XCD b % 8 through a ticket queue with per-(op, image)
-// completion counters (hand-offs stay in that XCD's L2) ----
-struct TeamOp {
-  ConvArgs a;                 // the layer's arguments exactly as its per-layer conv_deep launch
-  int var;                    // team_var(s2, mt, nb) (conv_deep.hip)
-  int items;                  // work items per image: n_tiles * Cout / nb
-  int toff;                   // column of the ResnetBlock's noise_func projection in the temb rows, -1: none
-  int dep;                    // op whose per-image completion this op waits for (-1: inputs precede the launch)
-  int pad[4];
-};
-struct TeamArgs {
-  const TeamOp* ops; int nops; int B;
-  unsigned* ctr;              // counters, one per kTeamSlot words: 8 team tickets, then done [nops][B];
-                              // zeroed before every launch (conv_in, ConvInArgs::zero)
-  unsigned* err;              // set to 1 when a dependency wait times out
-  const float* temb; int temb_ld; const int* t_dev; int temb_per_b;
-  const char* arena;          // base of the lane arena holding every activation / statistics tensor (< 4 GiB)
-  unsigned long long* stamps; // experiments (SDDM_TEAM_STAMPS): per item [xcc * 4096 + ticket][8] =
-                              // {op | b << 16, s_memrealtime at ticket, after the wait, at publish,
-                              //  staged, K loop done, stored, statistics written}
-};
-// nw = 4: two 4-wave workgroups per CU (64 per XCD); nw = 8: one 8-wave workgroup per CU (32 per XCD)
 // LDS per workgroup every launcher and planner sizes against: gfx950's 160 KiB (sddm_create fails
 // on a device that offers less, so no plan is built for LDS the device does not have)
 constexpr int kLdsBytes = 160 * 1024;
-constexpr int team_lds_budget(int nw) { return nw == 8 ? kLdsBytes : kLdsBytes / 2; }
-constexpr int kTeamSlot = 64;                 // words per team counter (256 bytes)
-hipError_t launch_conv_team(int dtype, int nw, const TeamArgs& a, int lds_bytes, int blocks, hipStream_t s);
-int conv_team_var(bool s2, int mt, int nb);  // -1: no team variant for this tiling
 
 // ---- row-streaming 3x3 convolution for segment widths 64 / 128 (conv_strip.hip) ----
 hipError_t launch_conv_strip(int dtype, int nblk, int mpi, int SR, const ConvArgs& a, int B, hipStream_t s);

@@ -145,11 +145,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   const int b = blockIdx.y, f0 = blockIdx.x * a.TR, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   if (a.t_dev && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.t_dev -= 1;
-  // zero the step's team-kernel counters (ticket lines + completion counters, conv_deep.hip): the
-  // team launch later in this step finds them zero (kernel boundary in between)
-  if (a.zero && blockIdx.x == 0 && blockIdx.y == 0)
-    for (int i = tid; i < a.nzero; i += 256) a.zero[(size_t)i * kTeamSlot] = 0u;
-  SDDM_STAMP(a, 0);
+  SDDM_STAMP_AT(a, 0, blockIdx.x + blockIdx.y * (a.F / a.TR));
   const int S = a.S, F = a.F, W = a.W, IW = W + 2, IH = a.TR + 2;
   {  // every load of the frame image issued before the first is stored (clamped addresses:
      // a load under a condition is waited for at the branch join)
@@ -213,7 +209,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
     }
   const float rW = 1.0f / (float)W;
   __syncthreads();                                        // frame image staged
-  SDDM_STAMP(a, 1);
+  SDDM_STAMP_AT(a, 1, blockIdx.x + blockIdx.y * (a.F / a.TR));
   const float* imgf = &img[0][0];
 #pragma unroll 2
   for (int fr = 0; fr < NFR; ++fr) {
@@ -265,7 +261,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
       store4p<T>(op + fc * 16 + 4 * g, d0 + bp[fc][0], d1 + bp[fc][1]);
     }
   }
-  SDDM_STAMP(a, 2);
+  SDDM_STAMP_AT(a, 2, blockIdx.x + blockIdx.y * (a.F / a.TR));
   // tile statistics: lanes of one channel group (xor 1..8) -> 4 waves (LDS), plain sums about the bias
 #pragma unroll
   for (int fc = 0; fc < 2; ++fc)
@@ -279,7 +275,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
       }
     }
   lds_sync();                                              // (the output stores stay in flight)
-  SDDM_STAMP(a, 3);
+  SDDM_STAMP_AT(a, 3, blockIdx.x + blockIdx.y * (a.F / a.TR));
   if (tid < CO) {
     const float n = (float)(a.TR * W);
     float S1 = 0.f, S2 = 0.f;
@@ -289,8 +285,8 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
     dst[0] = a.bias[tid] * n + S1;                 // sum
     dst[1] = fmaxf(S2 - S1 * S1 / n, 0.f);        // M2 about the tile mean
   }
-  SDDM_STAMP(a, 6);
-  SDDM_STAMP(a, 7);
+  SDDM_STAMP_AT(a, 6, blockIdx.x + blockIdx.y * (a.F / a.TR));
+  SDDM_STAMP_AT(a, 7, blockIdx.x + blockIdx.y * (a.F / a.TR));
 }
 
 hipError_t launch_conv_in(int dtype, const ConvInArgs& a, int B, hipStream_t s) {
@@ -381,7 +377,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
   float* P = (float*)smem;                    // [9][PR][PC]
   float* y = P + 9 * PR * PC;                 // [YR][W]
   float* gs = y + YR * W;                     // [2][C]
-  SDDM_STAMP(a, 0);
+  SDDM_STAMP_AT(a, 0, blockIdx.x + blockIdx.y * (a.F / a.FT));
   // every independent load first: the transition's x_t / condition (one 4-sample vector per
   // thread: the block's samples fit one pass, checked by the launcher), the GroupNorm statistics
   // and the first pass of activation fragments; then one wait
@@ -428,7 +424,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
   load_pass(wave);
   gl.finish(gf, b, C, 0, gs, gs + C);
   lds_sync();                                        // scale / shift visible (loads stay in flight)
-  SDDM_STAMP(a, 1);
+  SDDM_STAMP_AT(a, 1, blockIdx.x + blockIdx.y * (a.F / a.FT));
   // SiLU through exp2 with the constants folded: t = -(x sc + sh) log2(e) = x sc' + sh', and
   // silu = -ln2 * t / (1 + 2^t); the -ln2 goes into the fp32 weights (one multiply per lane)
   constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
@@ -486,7 +482,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
   }
   }
   lds_sync();
-  SDDM_STAMP(a, 2);
+  SDDM_STAMP_AT(a, 2, blockIdx.x + blockIdx.y * (a.F / a.FT));
   for (int p = tid; p < YR * W; p += NT) {
     const int r = p / W, w = p - r * W;        // y row r <-> P rows r .. r+2, cols w .. w+2
     float s = 0.f;
@@ -497,7 +493,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
     y[p] = s + a.bias;
   }
   lds_sync();
-  SDDM_STAMP(a, 3);
+  SDDM_STAMP_AT(a, 3, blockIdx.x + blockIdx.y * (a.F / a.FT));
   const int t = a.t_dev ? *a.t_dev : 0;
   const uint64_t seed = a.sp ? a.sp->seed : a.seed;
   const int64_t row_offset = a.sp ? a.sp->row_offset : a.row_offset;
@@ -546,8 +542,8 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
         for (int j = 0; j < 4 && n4 + j < n_end; ++j) xrow[n4 + j] = o[j];
     }
   }
-  SDDM_STAMP(a, 6);
-  SDDM_STAMP(a, 7);
+  SDDM_STAMP_AT(a, 6, blockIdx.x + blockIdx.y * (a.F / a.FT));
+  SDDM_STAMP_AT(a, 7, blockIdx.x + blockIdx.y * (a.F / a.FT));
 }
 
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {

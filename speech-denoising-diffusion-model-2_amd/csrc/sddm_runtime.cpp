@@ -228,7 +228,6 @@ struct RunState {  // fields patched into the plan's kernel arguments at launch 
   int64_t noise_ld = 0;
 };
 
-static constexpr int kTeamDefault = 0;  // deep-level team kernel off until it beats the per-layer launches
 static constexpr int kStreams = 4;    // concurrent lane streams (GPU_MAX_HW_QUEUES is 4)
 static constexpr int kMaxLanes = 64;  // step counters reserved in the weight arena
 
@@ -238,7 +237,6 @@ struct Lane {                         // one row block of the batch: plan + acti
   std::vector<Op> ops;
   RunState rs;
   size_t off_temb_fwd = 0, off_cond = 0, off_x = 0;
-  unsigned* team_err = nullptr;       // team kernel's wait-timeout word (zeroed at plan build)
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   int g_K = 0, g_gen = -1;
@@ -301,11 +299,6 @@ struct sddm_ctx {
   struct KernTune { int kind, a, b, c; };
   std::map<std::string, KernTune> kern_tune;
   int tune_B = -1, tune_dtype = -1, tune_N = -1;
-  // deep-level team kernel (conv_deep.hip conv_team_kernel): the consecutive 16-bit convolutions
-  // whose outputs have at most team_px pixels run as one launch per step (tuning JSON keys "team":
-  // 0 off, 1 on, 2 team tilings as per-layer launches, and "team_px"; SDDM_TEAM, SDDM_TEAM_PX override)
-  int team = kTeamDefault;
-  int team_px = 512;
   int hop_samples = 256;
 
   const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
@@ -503,7 +496,6 @@ struct ConvChoice {
   int nblk = 32, SR = 0, mpi = 128;
   int mt = 0, ckb = 0, nw = 4, nb = 32;           // conv_deep: pixels per block, input chunks, waves, channels
   int tile = -1;                                  // conv_tile configuration (16-bit dtypes), -1: none
-  int team = 0;                                   // conv_deep tiling chosen for the team kernel (nw = 4)
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
 };
 
@@ -559,57 +551,6 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
   ch.strip = 0; ch.mt = pick->mt; ch.nw = pick->nw; ch.nb = nb; ch.ckb = (a.CA + a.CB) / 32;
   ch.TR = pick->TR; ch.TW = pick->TW; ch.tiles_x = pick->tiles_x; ch.n_tiles = pick->n_tiles;
   return true;
-}
-
-// conv_deep tiling of a layer run by the team kernel (conv_team_kernel): 4 waves, 16 or 32 output
-// channels, LDS within two workgroups per CU.  A team is one XCD (64 workgroups) serving
-// ceil(PB / 8) images; per candidate the op's time is estimated as the larger of (rounds of
-// items x one item's latency: its L2 bytes at ~64 B/clk into one CU + its MFMA cycles + a fixed
-// ~1500 clk of hand-off and round trips) and the team's L2 bytes at ~2 KB/clk.  SDDM_TEAM_CFG=mt:nb
-// forces a tiling wherever it fits (experiments).
-static bool choose_team(int dt, int PB, int nw, int Cin, int RC, int res_mode, int Ho, int Wo, int Cout, bool s2, bool up,
-                        ConvChoice& ch) {
-  static int f_mt = -1, f_nb = 0;
-  if (f_mt < 0) {
-    f_mt = 0;
-    if (const char* e = std::getenv("SDDM_TEAM_CFG")) std::sscanf(e, "%d:%d", &f_mt, &f_nb);
-  }
-  if (dt == DT_F32 || Cin % 32 || RC % 32 || Cout % 16) return false;
-  ConvArgs a{};
-  a.CA = Cin; a.RCA = RC; a.res_mode = res_mode; a.Ho = Ho; a.Wo = Wo; a.Cout = Cout; a.upsample = up ? 1 : 0;
-  a.Hi = up ? Ho / 2 : (s2 ? Ho * 2 : Ho); a.Wi = up ? Wo / 2 : (s2 ? Wo * 2 : Wo);
-  a.deep_nw = nw;
-  const int nimg = (PB + 7) / 8, es = 2, K = 9 * Cin + (res_mode == 2 ? RC : 0);
-  const double wgs = 32.0 * 8 / nw;              // workgroups of a team
-  double best = 1e30;
-  bool found = false;
-  for (int mt : {32, 64, 128})
-    for (int nb : {16, 32}) {
-      if (conv_team_var(s2, mt, nb) < 0 || Cout % nb) continue;
-      if (nw == 8 && s2 && nb == 16) continue;     // no per-layer conv_deep of that shape (team mode 2 reference)
-      if (f_mt && (mt != f_mt || nb != f_nb)) continue;
-      const int TW = std::min(Wo, mt);
-      if (mt % TW || Wo % TW) continue;
-      const int TR = std::min(mt / TW, Ho);
-      if (Ho % TR || (TR * TW < mt && mt > 32)) continue;
-      a.TR = TR; a.TW = TW; a.tiles_x = Wo / TW; a.n_tiles = a.tiles_x * (Ho / TR); a.deep_nb = nb;
-      if (conv_deep_lds_bytes(dt, mt, s2, a) > (size_t)team_lds_budget(nw)) continue;
-      const double halo = s2 ? (2.0 * TR + 1) * (2 * TW + 1) : (TR + 2.0) * (TW + 2);
-      const double item_bytes = (double)nb * K * es + halo * Cin * es + (res_mode == 2 ? (double)TR * TW * RC * es : 0) +
-                                (double)TR * TW * nb * es * (res_mode == 1 ? 2 : 1);
-      const double items = (double)a.n_tiles * (Cout / nb) * nimg;
-      const double mfma = (mt / 16.0) * (nb / 16.0) * (K / 32.0) * 8.0 / 4.0;
-      const double rounds = std::ceil(items / wgs);
-      const double cost = std::max(rounds * (item_bytes / 64.0 + mfma + 1500.0), items * item_bytes / 2048.0);
-      if (cost < best) {
-        best = cost;
-        found = true;
-        ch = ConvChoice{};
-        ch.strip = 0; ch.mt = mt; ch.nw = nw; ch.nb = nb; ch.ckb = Cin / 32; ch.team = 1;
-        ch.TR = TR; ch.TW = TW; ch.tiles_x = a.tiles_x; ch.n_tiles = a.n_tiles;
-      }
-    }
-  return found;
 }
 
 // conv_tile configuration: the largest pixel x channel tile (most reuse of each transformed input
@@ -730,7 +671,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   L.off_cond = A.reserve(sizeof(float) * (size_t)B * N);
   L.off_x = A.reserve(sizeof(float) * (size_t)B * N);
 
-  enum { ST_CONVIN, ST_GN, ST_CONV, ST_FINAL, ST_TEAM };
+  enum { ST_CONVIN, ST_GN, ST_CONV, ST_FINAL };
   struct Step {
     int type = 0;
     std::string w;          // weight-name prefix
@@ -739,17 +680,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
     int s2 = 0, up = 0, res_mode = 0, rawA = -1, rawB = -1, cout = 0;
     bool temb = false;
     ConvChoice ch;
-    int team = -1;          // ST_TEAM: index into teams
   };
-  // deep-level team launches (conv_team_kernel): the conv steps each one runs, its op table
-  struct TeamPlan {
-    std::vector<Step> steps;
-    size_t off_ops = 0;
-    size_t ctr_word = 0;    // first counter word of this team in the step's counter block
-  };
-  std::vector<TeamPlan> teams;
-  size_t off_err = 0, off_ctr = 0;
-  int n_ctr = 0;            // counter words conv_in clears every step
   std::vector<Step> prog;
   // measured per-layer deep tiles (sddm_set_conv_tuning) apply when they were measured for this
   // lane batch, dtype and length; otherwise the round-count heuristic of choose_deep decides
@@ -758,16 +689,6 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   // and GroupNorm tilings, hence bit-identical rows
   const int PB = std::max(1, c->lane_rows);
   const bool tuned = c->tune_B == PB && c->tune_dtype == dt && c->tune_N == N;
-  // the team kernel spreads a lane's images over the 8 XCDs: on by default for 16-bit lanes of 8+
-  // rows (SDDM_TEAM=1 forces it for any lane, SDDM_TEAM=0 turns it off)
-  static const char* env_team = std::getenv("SDDM_TEAM");
-  static const int env_team_px = std::getenv("SDDM_TEAM_PX") ? std::atoi(std::getenv("SDDM_TEAM_PX")) : 0;
-  // (mode 2: the team tilings, each layer still its own conv_deep launch: the bit-exact reference the
-  // tests compare the team launch with)
-  const int team_mode = env_team ? std::atoi(env_team) : c->team;
-  const bool team_on = dt != DT_F32 && team_mode != 0 && (env_team != nullptr || PB >= 8);
-  const int team_px = env_team_px > 0 ? env_team_px : c->team_px;
-  constexpr int team_nw = 8;   // 8-wave team items (the 4-wave variant measured slower)
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
     int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;
@@ -780,7 +701,6 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         if (kind == 3) { wm = kt->second.a; wn = kt->second.b; wb = kt->second.c; }
       }
     }
-    if (team_on && Ho * Wo <= team_px && choose_team(dt, PB, team_nw, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch)) return true;
     return choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka, wb);
   };
   const int TRin = 512 / W;
@@ -850,37 +770,6 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   const int gf = new_gn(cur, -1, "final_conv");
   { Step st; st.type = ST_FINAL; st.srcA = cur; st.gn = gf; prog.push_back(st); }
 
-  // ---- deep-level team launches: every run of >= 2 consecutive team-tiled conv steps becomes one
-  // conv_team_kernel launch (a lone one runs as its per-layer conv_deep launch, same tiling) ----
-  {
-    std::vector<Step> np;
-    for (size_t i = 0; i < prog.size();) {
-      size_t j = i;
-      while (j < prog.size() && prog[j].type == ST_CONV && prog[j].ch.team) ++j;
-      if (j - i >= 2 && team_mode != 2 && A.used < ((size_t)1 << 32)) {   // hand-off loads address the arena with 32-bit offsets
-        TeamPlan tp;
-        tp.steps.assign(prog.begin() + i, prog.begin() + j);
-        tp.off_ops = A.reserve(sizeof(TeamOp) * tp.steps.size());
-        tp.ctr_word = (size_t)n_ctr;
-        n_ctr += 8 + (int)tp.steps.size() * B;            // counters (kTeamSlot words each)
-        Step ts;
-        ts.type = ST_TEAM;
-        ts.team = (int)teams.size();
-        teams.push_back(tp);
-        np.push_back(ts);
-        i = j;
-      } else if (j > i) {
-        for (; i < j; ++i) np.push_back(prog[i]);
-      } else {
-        np.push_back(prog[i++]);
-      }
-    }
-    prog.swap(np);
-    if (!teams.empty()) {
-      off_err = A.reserve(256);
-      off_ctr = A.reserve(sizeof(unsigned) * kTeamSlot * (size_t)n_ctr);
-    }
-  }
   SDDM_HIP_CHECK(A.commit());
 
   // ---- pass 2: materialise kernel arguments ----
@@ -894,7 +783,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   };
   auto WF = [&](const std::string& k) { return c->warena.at<float>(c->woff.at(k)); };
   auto WV = [&](const std::string& k) { return (const void*)(c->warena.base + c->woff.at(k)); };
-  // the kernel arguments of one conv step (per-layer launch or team op), its algorithmic bytes and FLOPs
+  // the kernel arguments of one conv step, its algorithmic bytes and FLOPs
   auto conv_args = [&](const Step& st, ConvArgs& a, double& bytes, double& flops) -> int {
     a = ConvArgs{};
     const Tensor sa = TT(st.srcA), sb = TT(st.srcB), o = TT(st.out);
@@ -946,7 +835,6 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       a.w = WF("downs.0.weight"); a.bias = WF("downs.0.bias");
       const Tensor o = TT(st.out);
       a.out = o.p; a.stats = o.stats; a.TR = TRin;
-      if (n_ctr) { a.zero = A.at<unsigned>(off_ctr); a.nzero = n_ctr; }
       const double bytes = (double)B * N * 4 * 2 + (double)B * F * W * u.inner * es;
       const double flops = 2.0 * B * F * W * u.inner * 18;
 #ifdef SDDM_STAMPS
@@ -1043,57 +931,6 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         };
         (void)base;
       }
-    } else if (st.type == ST_TEAM) {
-      TeamPlan& tp = teams[st.team];
-      std::vector<TeamOp> ops(tp.steps.size());
-      double bytes = 0, flops = 0;
-      int lds = 0;
-      for (size_t i = 0; i < tp.steps.size(); ++i) {
-        const Step& ms = tp.steps[i];
-        TeamOp& o = ops[i];
-        o = TeamOp{};
-        double by = 0, fl = 0;
-        if (const int r = conv_args(ms, o.a, by, fl)) return r;
-        bytes += by; flops += fl;
-        o.a.deep_nw = ms.ch.nw; o.a.deep_nb = ms.ch.nb; o.a.ck_batch = ms.ch.ckb;
-        o.var = conv_team_var(ms.s2 != 0, ms.ch.mt, ms.ch.nb);
-        if (o.var < 0) FAIL(SDDM_ERR_STATE, "no team variant for %s", ms.w.c_str());
-        o.items = o.a.n_tiles * (o.a.Cout / ms.ch.nb);
-        o.toff = ms.temb ? c->temb_off.at(ms.rb) : -1;
-        o.dep = (int)i - 1;            // every op reads its predecessor's output
-        static const int team_dbg = std::getenv("SDDM_TEAM_DBG") ? std::atoi(std::getenv("SDDM_TEAM_DBG")) : 0;
-        o.a.dbg = team_dbg;            // ablation bits of conv_deep (timing experiments only)
-        lds = std::max(lds, (int)conv_deep_lds_bytes(dt, ms.ch.mt, ms.s2 != 0, o.a));
-        if (std::getenv("SDDM_PLAN_DEBUG"))
-          fprintf(stderr, "team op %zu %s: mt %d nb %d tiles %d items/img %d Cin %d Cout %d gn tiles %d+%d lds %zu\n", i,
-                  ms.w.c_str(), ms.ch.mt, ms.ch.nb, o.a.n_tiles, o.items, o.a.CA + o.a.CB, o.a.Cout, o.a.gtilesA,
-                  o.a.gtilesB, conv_deep_lds_bytes(dt, ms.ch.mt, ms.s2 != 0, o.a));
-      }
-      const int tnw = tp.steps.front().ch.nw;
-      if (lds > team_lds_budget(tnw)) FAIL(SDDM_ERR_STATE, "team LDS %d bytes", lds);
-      SDDM_HIP_CHECK(hipMemcpy(A.base + tp.off_ops, ops.data(), sizeof(TeamOp) * ops.size(), hipMemcpyHostToDevice));
-      SDDM_HIP_CHECK(hipMemset(A.base + off_err, 0, 256));
-      TeamArgs ta{};
-      ta.ops = A.at<TeamOp>(tp.off_ops); ta.nops = (int)ops.size(); ta.B = B;
-      ta.ctr = A.at<unsigned>(off_ctr) + tp.ctr_word * kTeamSlot; ta.err = A.at<unsigned>(off_err);
-      ta.arena = (const char*)A.base;
-      if (std::getenv("SDDM_TEAM_STAMPS")) {   // per-item timestamps (experiments; sddm_debug_stamps)
-        if (!c->stamp_buf) SDDM_HIP_CHECK(hipMalloc(&c->stamp_buf, sizeof(unsigned long long) * 8 * 65536));
-        SDDM_HIP_CHECK(hipMemset(c->stamp_buf, 0, sizeof(unsigned long long) * 8 * 65536));
-        ta.stamps = c->stamp_buf;
-        c->stamp_blocks = 8 * 4096;          // [8 teams][4096 tickets][8 words]
-      }
-      const int blocks = 8 * 32 * 8 / tnw;   // 4 waves: two workgroups on each of an XCD's 32 CUs; 8 waves: one
-      const std::string nm = "team[" + tp.steps.front().w + ".." + tp.steps.back().w + "]";
-      L.ops.push_back({2, bytes, flops, [ctx, lp, ta, lds, blocks, dt, tnw](hipStream_t s) {
-                          TeamArgs x = ta;
-                          x.temb = lp->rs.temb; x.temb_ld = ctx->SC; x.t_dev = lp->rs.t_dev;
-                          x.temb_per_b = lp->rs.temb_per_b;
-                          return launch_conv_team(dt, tnw, x, lds, blocks, s);
-                        }, nm});
-      L.ops.back().kname = std::string("conv_team_kernel<") + dt_name(dt) + "," + std::to_string(tnw) + ">";
-      L.ops.back().kinst = L.ops.back().kname;
-      L.team_err = ta.err;
     } else {
       FinalArgs f{};
       const Tensor src = TT(st.srcA);
@@ -1192,21 +1029,6 @@ static int prof_drain(sddm_ctx* c, const Lane& L) {
     a.ms += m; a.n += 1; a.bytes += L.ops[pe.first].bytes; a.flops += L.ops[pe.first].flops;
   }
   c->ev_pend.clear();
-  return SDDM_OK;
-}
-
-// SDDM_TEAM_CHECK=1 (tests): after a call, wait for it and fail if a team kernel's dependency wait
-// timed out (its results would be wrong; the kernel never hangs)
-static int team_check(sddm_ctx* c, hipStream_t s) {
-  const char* e = std::getenv("SDDM_TEAM_CHECK");
-  if (!e || std::atoi(e) == 0) return SDDM_OK;
-  SDDM_HIP_CHECK(hipStreamSynchronize(s));
-  for (auto& Lp : c->lanes)
-    if (Lp->team_err) {
-      unsigned e = 0;
-      SDDM_HIP_CHECK(hipMemcpy(&e, Lp->team_err, sizeof(e), hipMemcpyDeviceToHost));
-      if (e) FAIL(SDDM_ERR_HIP, "team kernel dependency wait timed out (lane %d)", Lp->idx);
-    }
   return SDDM_OK;
 }
 
@@ -1632,7 +1454,7 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
       SDDM_HIP_CHECK(hipEventRecord(c->ev_done[k], c->work[k]));
       SDDM_HIP_CHECK(hipStreamWaitEvent(user, c->ev_done[k], 0));
     }
-    return team_check(c, user);
+    return SDDM_OK;
   }
   int64_t nrec = 0;
   for (int t = T; t >= 1; --t) {
@@ -1645,7 +1467,7 @@ static int sample_impl(sddm_ctx* c, const float* cond, int64_t B, int64_t N, uin
       ++nrec;
     }
   }
-  return team_check(c, user);
+  return SDDM_OK;
 }
 
 int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const float* noise_level, int64_t B,
@@ -1676,7 +1498,7 @@ int sddm_network_forward(sddm_ctx* c, const float* cond, const float* x_t, const
     r = run_ops(c, L, s);
     if (r) return r;
   }
-  return team_check(c, s);
+  return SDDM_OK;
 }
 
 int sddm_transition(sddm_ctx* c, int mode, const float* x_t, const float* eps, const float* cond, int t, int64_t B,
@@ -1764,8 +1586,6 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
       if (t.kind == 2 && (t.a < 0 || t.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), t.a);
       c->kern_tune[kv.first] = t;
     }
-  c->team = (int)j.number("team", kTeamDefault);
-  c->team_px = (int)j.number("team_px", 512);
   c->tune_B = (int)j.number("lane_batch", -1);
   c->tune_dtype = dt;
   c->tune_N = (int)j.number("num_samples", -1);

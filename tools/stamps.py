@@ -3,8 +3,8 @@
     SDDM_BUILD_VARIANT=stamps python speech-denoising-diffusion-model-2_amd/sddm_hip/build.py
     python tools/stamps.py [--batch 16] [--dtype bf16] op1 op2 ...
 
-Stamps (conv_common.h SDDM_STAMP): slot 0 / 7 = s_memrealtime (100 MHz) at block start / end,
-slots 1..6 = s_memtime at phase boundaries (deep kernel: 1 staging loads issued, 2 GroupNorm
+Stamps (conv_common.h SDDM_STAMP): s_memrealtime (100 MHz) at block start (0), end (7) and
+the phase boundaries (1..6) (deep kernel: 1 staging loads issued, 2 GroupNorm
 finalized, 3 LDS image written, 4 K loop done, 5 epilogue stored, 6 stats written; strip kernel:
 3 initial rows staged, 4 row loop done, 6 stats written).
 """
@@ -65,9 +65,8 @@ def main():
         span = (t7.max() - t0.min()) * 10e-3
         dur = (t7 - t0) * 10e-3
         start = (t0 - t0.min()) * 10e-3
-        nz = [k for k in range(1, 7) if st[:, k].any()]
-        ph = [f"{k0}->{k1}: {np.mean(st[:, k1] - st[:, k0]):8.0f}" for k0, k1 in zip(nz[:-1], nz[1:])]
-        cyc = st[:, 6] - st[:, 1] if st[:, 1].any() else st[:, 6] - st[:, 3]
+        nz = [0] + [k for k in range(1, 7) if st[:, k].any()] + [7]
+        ph = [f"{k0}->{k1}: {np.mean(st[:, k1] - st[:, k0]) * 10e-3:6.2f}" for k0, k1 in zip(nz[:-1], nz[1:])]
         ev = sorted([(x, 1) for x in t0] + [(x, -1) for x in t7], key=lambda e: (e[0], e[1]))
         cur = conc = 0
         for _, d in ev:
@@ -75,7 +74,7 @@ def main():
             conc = max(conc, cur)
         print(f"{op}: {n.value} blocks, span {span:.1f} us, block dur mean {dur.mean():.2f} max {dur.max():.2f} us, "
               f"start spread max {start.max():.2f} us (p50 {np.median(start):.2f}), max concurrent blocks {conc}")
-        print("   cycles " + "  ".join(ph) + f"   (sum {cyc.mean():.0f} cyc)")
+        print("   us " + "  ".join(ph))
         ctx.close()
 
 
