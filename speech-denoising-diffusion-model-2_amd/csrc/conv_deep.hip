@@ -35,7 +35,15 @@ namespace sddm {
 // 16 zero bytes for the halo pixels outside the image (LDS-DMA has no zero fill)
 __device__ __attribute__((aligned(256))) unsigned char g_deep_zero[256];
 
-constexpr int kDeepMaxChunks = 10;   // 64-pixel chunks of a halo plane (640 halo pixels)
+constexpr int kDeepMaxChunks = 10;
+
+// timing ablations of the profiling build (SDDM_STAMPS_DBG; results are garbage under any flag):
+// 4 no halo DMA, 32 no weight loads
+#ifdef SDDM_STAMPS
+#define SDDM_DEEP_DBG(bit) ((a.dbg & (bit)) != 0)
+#else
+#define SDDM_DEEP_DBG(bit) false
+#endif   // 64-pixel chunks of a halo plane (640 halo pixels)
 
 struct DeepGeo { int HR, HC, HP, NCH, PLB, NCR, PLR; };
 
@@ -136,7 +144,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 #pragma unroll
   for (int d = 0; d < D; ++d)
 #pragma unroll
-    for (int fc = 0; fc < FC; ++fc) wa[d][fc] = wfrag(min(wv + NW * d, s_last), fc);
+    for (int fc = 0; fc < FC; ++fc) wa[d][fc] = SDDM_DEEP_DBG(32) ? Frag<T>{} : wfrag(min(wv + NW * d, s_last), fc);
   // (c) identity residual of this thread's epilogue pixels (4 channels each, clamped: unconditional)
   f32x4 idr[EIT];
   {
@@ -150,41 +158,37 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   }
   // (d) the input halo by LDS-DMA, last: its loops issue a block-dependent number of DMAs, and
   // a register load issued after them would be waited for with vmcnt(0) (the compiler cannot
-  // count them); everything above is straight-line, so its waits stay exact.  This lane's pixel
-  // of every 64-pixel chunk (index of the source pixel, -1 outside the image), then one DMA per
-  // (chunk, plane)
-  int pxo[kDeepMaxChunks];
-  const float rHC = 1.0f / (float)HC;
-#pragma unroll
-  for (int r = 0; r < kDeepMaxChunks; ++r) {
-    pxo[r] = -1;
-    if (r >= geo.NCH) continue;                          // block-uniform
-    const int hp = r * 64 + lane, hy = fdivi(hp, rHC), hx = hp - hy * HC;
-    int iy, ix;
-    bool ok;
-    if (S2) {
-      iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
-      ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
-    } else {
-      iy = y0 - 1 + hy; ix = x0 - 1 + hx;
-      ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
-      if (a.upsample) { iy >>= 1; ix >>= 1; }
-    }
-    pxo[r] = (ok && hp < geo.HP) ? iy * a.Wi + ix : -1;
-  }
+  // count them); everything above is straight-line, so its waits stay exact.  Per 64-pixel chunk
+  // r: this lane's halo pixel -> source pixel (computed once, reused for every plane), then one
+  // DMA per plane of this wave; bit r of `inb`: the pixel lies inside the image
   auto dma = [&](const char* src, char* dst) {
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)dst, 16, 0, 0);
   };
-#pragma unroll
-  for (int r = 0; r < kDeepMaxChunks; ++r) {
-    if (r < geo.NCH) {                                   // block-uniform
-      const int pix = pxo[r];
-      const unsigned oa = (unsigned)pix * (unsigned)(a.CA * ES), ob = (unsigned)pix * (unsigned)(a.CB * ES);
-      for (int q = wv; q < npl; q += NW) {               // wave-uniform planes
-        const char* src = q < plA ? srcA + oa + q * 16 : srcB + ob + (q - plA) * 16;
-        dma(pix >= 0 ? src : zero, smem + q * PLB + r * 1024);
+  unsigned inb = 0;
+  {
+    const float rHC = 1.0f / (float)HC;
+    for (int r = 0; r < geo.NCH; ++r) {                  // block-uniform
+      const int hp = r * 64 + lane, hy = fdivi(hp, rHC), hx = hp - hy * HC;
+      int iy, ix;
+      bool ok;
+      if (S2) {
+        iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
+        ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+      } else {
+        iy = y0 - 1 + hy; ix = x0 - 1 + hx;
+        ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
+        if (a.upsample) { iy >>= 1; ix >>= 1; }
       }
+      ok = ok && hp < geo.HP;
+      inb |= ok ? 1u << r : 0u;
+      const unsigned pix = ok ? (unsigned)(iy * a.Wi + ix) : 0u;
+      const char* pa = ok ? srcA + pix * (unsigned)(a.CA * ES) : zero;
+      const char* pb = ok ? srcB + pix * (unsigned)(a.CB * ES) - plA * 16 : zero;
+      const unsigned step = ok ? 16u : 0u;               // the zero page for every plane outside
+      char* dl = smem + r * 1024;
+      for (int q = wv; q < npl; q += NW)                 // wave-uniform planes
+        if (!SDDM_DEEP_DBG(4)) dma((q < plA ? pa : pb) + q * step, dl + q * PLB);
     }
   }
   // (e) the res_conv input at the output pixels (1x1, raw concat)
@@ -232,9 +236,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 #pragma unroll
         for (int i = 0; i < 4; ++i) { s[j + i] = x[i]; h[j + i] = y[i]; }
       }
-#pragma unroll
-      for (int r = 0; r < kDeepMaxChunks; ++r) {
-        if (r < geo.NCH && pxo[r] >= 0) {
+      for (int r = 0; r < geo.NCH; ++r) {
+        if ((inb >> r) & 1u) {
           f32x4* p = (f32x4*)(smem + q * PLB + r * 1024 + lane * 16);
           *p = transform_regs<T>(*p, s, h);
         }
