@@ -228,18 +228,27 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
 
   // ---------------- 3. GroupNorm + SiLU in place (zero padding stays zero) ----------------
   if (gn) {
-    for (int q = wv; q < npl; q += NW) {
-      float s[VE], h[VE];
+    // two planes per pass (the second clamped to the first when the wave has an odd count), so
+    // the LDS round trips of one overlap the transcendentals of the other
+    for (int q0 = wv; q0 < npl; q0 += 2 * NW) {
+      const bool two = q0 + NW < npl;                    // wave-uniform
+      const int q1 = two ? q0 + NW : q0;
+      float s0[VE], h0[VE], s1[VE], h1[VE];
 #pragma unroll
       for (int j = 0; j < VE; j += 4) {                  // wave-uniform (broadcast) reads
-        const f32x4 x = *(const f32x4*)(gsc + q * VE + j), y = *(const f32x4*)(gsc + Cin + q * VE + j);
+        const f32x4 x0 = *(const f32x4*)(gsc + q0 * VE + j), y0 = *(const f32x4*)(gsc + Cin + q0 * VE + j);
+        const f32x4 x1 = *(const f32x4*)(gsc + q1 * VE + j), y1 = *(const f32x4*)(gsc + Cin + q1 * VE + j);
 #pragma unroll
-        for (int i = 0; i < 4; ++i) { s[j + i] = x[i]; h[j + i] = y[i]; }
+        for (int i = 0; i < 4; ++i) { s0[j + i] = x0[i]; h0[j + i] = y0[i]; s1[j + i] = x1[i]; h1[j + i] = y1[i]; }
       }
       for (int r = 0; r < geo.NCH; ++r) {
         if ((inb >> r) & 1u) {
-          f32x4* p = (f32x4*)(smem + q * PLB + r * 1024 + lane * 16);
-          *p = transform_regs<T>(*p, s, h);
+          f32x4* p0 = (f32x4*)(smem + q0 * PLB + r * 1024 + lane * 16);
+          f32x4* p1 = (f32x4*)(smem + q1 * PLB + r * 1024 + lane * 16);
+          const f32x4 v0 = *p0, v1 = *p1;
+          const f32x4 o0 = transform_regs<T>(v0, s0, h0), o1 = transform_regs<T>(v1, s1, h1);
+          *p0 = o0;
+          if (two) *p1 = o1;
         }
       }
     }
