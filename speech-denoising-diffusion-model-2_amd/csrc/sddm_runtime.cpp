@@ -688,7 +688,9 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   // every lane, and every row partition of a batch (sharded runs), gets the same kernels, tiles
   // and GroupNorm tilings, hence bit-identical rows
   const int PB = std::max(1, c->lane_rows);
-  const bool tuned = c->tune_B == PB && c->tune_dtype == dt && c->tune_N == N;
+  // (a table measured in bf16 also serves f16: the same kernels at the same bytes and MFMA rate)
+  const bool same_dt = c->tune_dtype == dt || (c->tune_dtype >= 0 && c->tune_dtype != DT_F32 && dt != DT_F32);
+  const bool tuned = c->tune_B == PB && same_dt && c->tune_N == N;
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
     int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;

@@ -176,7 +176,7 @@ class SDDM_spectrogram(SDDM):
 def _noise_buffer(noise, T, out):
     """Caller noise as the contiguous fp32 [T + 1][B][N] device buffer of sddm_sample_noise."""
     n = torch.as_tensor(noise)
-    if n.shape[0] != T + 1 or n[0].numel() != out.numel():
+    if tuple(n.shape) != (T + 1,) + tuple(out.shape):
         raise ValueError(f"noise must be [T + 1 = {T + 1}, {tuple(out.shape)}], got {tuple(n.shape)}")
     return n.to(device=out.device, dtype=torch.float32).contiguous()
 

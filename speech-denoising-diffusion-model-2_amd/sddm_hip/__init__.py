@@ -114,6 +114,7 @@ class Context:
         check(lib().sddm_create(self.device, self.dtype, ctypes.byref(h)))
         self._h = h
         check(lib().sddm_configure(self._h, json.dumps(config).encode()))
+        self.timesteps = int(config.get("diffusion", {}).get("args", {}).get("n_timestep", 0)) or None
 
     def close(self):
         if getattr(self, "_h", None):
@@ -150,9 +151,19 @@ class Context:
                                 _ptr(out), _stream(torch, cond.device)))
 
     def sample_noise(self, cond, out, noise):
-        """sddm_sample_noise: every Gaussian draw from `noise` ([T + 1][B][N] fp32 on the device)."""
+        """sddm_sample_noise: every Gaussian draw from `noise` ([T + 1][B][N] fp32 on the device).
+        The library reads (T + 1) * B * N floats from that pointer, so the buffer is checked here:
+        a contiguous fp32 device tensor of shape (T + 1, B, ...) holding exactly that many values."""
         import torch
         B, N = out.shape[0], out.shape[-1]
+        T = self.timesteps
+        if not isinstance(noise, torch.Tensor) or noise.dtype != torch.float32 or not noise.is_contiguous():
+            raise ValueError("noise must be a contiguous float32 tensor")
+        if noise.device != out.device:
+            raise ValueError(f"noise must be on {out.device}, got {noise.device}")
+        if noise.dim() < 2 or noise.shape[1] != B or (T is not None and noise.shape[0] != T + 1) or \
+                noise.numel() != noise.shape[0] * B * N:
+            raise ValueError(f"noise must be [T + 1, {B}, {N}] draws, got {tuple(noise.shape)}")
         check(lib().sddm_sample_noise(self._h, _ptr(cond), B, N, _ptr(noise), _ptr(out), _stream(torch, cond.device)))
 
     def sample_continuous(self, cond, out, record, sample_inter, seed, row_offset=0):

@@ -86,3 +86,61 @@ def test_reference_noise_layout_and_errors(torch_cuda):
     net.load_state_dict({k: torch.from_numpy(v) for k, v in unet_params(N).items()})
     with pytest.raises(ValueError):
         m.infer(cond.cuda(), noise=torch.zeros(3, 2, 1, N))
+
+
+def test_unet_caller_noise_across_lanes(torch_cuda):
+    """Caller noise with B larger than the lane (lane_rows = 2, B = 4: two lanes, each reading its rows
+    of every draw at noise + row0 * N with stride B * N, final_kernel's vector noise loads included):
+    the HIP loop equals the oracle fed the same draws (fp32, T=3, distinct rows)."""
+    import model.diffusion as D
+    import model.model as M
+    import model.network as NW
+    from oracle import sampler, unet
+    from oracle.schedule import BUFFER_NAMES
+    from sddm_hip.synth import noisy_speech
+    N, B, sched = 2112, 4, ("linear", 3, 1e-4, 0.05)
+    dev = torch.device("cuda", 0)
+    P = unet_params(N)
+    net = NW.UNetModified2(num_samples=N, **UNET_NET["args"])
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    d = D.GaussianDiffusion(*sched, device=dev)
+    m = M.SDDM(d, net, p_transition="original").to(dev)
+    m.lane_rows = 2
+    cond = noisy_speech(B, N, seed=11)
+    noise = np.random.default_rng(5).standard_normal((sched[1] + 1, B, 1, N)).astype(np.float32)
+    out = m.infer(torch.from_numpy(cond).to(dev), noise=torch.from_numpy(noise)).cpu().numpy()
+    tab = {k: getattr(d, k).cpu().numpy() for k in BUFFER_NAMES}
+    arch = unet.architecture(N, inner_channel=32, channel_mults=(1, 2, 3, 4, 5), res_blocks=1)
+    ref = sampler.infer(lambda c, x, nl: unet.forward(P, arch, c, x, nl), tab, cond, "original", noise=noise)
+    errs = [rms(out[b], ref[b]) for b in range(B)]
+    print(f"caller noise, 2-row lanes x 2: row rms {' '.join(f'{e:.2e}' for e in errs)}")
+    assert np.isfinite(out).all() and max(errs) <= 1e-5
+
+
+def test_wavegrad_caller_noise_matches_oracle(torch_cuda):
+    """SDDM_spectrogram.infer + WaveGrad with caller draws (sddm_sample_noise on the WaveGrad loop)
+    equals the oracle's infer_spectrogram fed the same draws (fp32, T=3, B=2, 6 frames)."""
+    import model.diffusion as D
+    import model.model as M
+    import model.network as NW
+    from oracle import sampler
+    from oracle import wavegrad as wg
+    from oracle.schedule import BUFFER_NAMES
+    from _helpers import wavegrad_params
+    sched = ("linear", 3, 1e-4, 0.05)
+    dev = torch.device("cuda", 0)
+    P = wavegrad_params()
+    net = NW.WaveGrad()
+    net.load_state_dict({k: torch.from_numpy(v) for k, v in P.items()})
+    d = D.GaussianDiffusion(*sched, device=dev)
+    m = M.SDDM_spectrogram(d, net.to(dev), hop_samples=300).to(dev)
+    rng = np.random.default_rng(9)
+    spec = rng.uniform(0, 1, (2, 128, 6)).astype(np.float32)
+    noise = rng.standard_normal((sched[1] + 1, 2, 1, 300 * 6)).astype(np.float32)
+    out = m.infer(torch.from_numpy(spec).to(dev), noise=torch.from_numpy(noise)).cpu().numpy()
+    tab = {k: getattr(d, k).cpu().numpy() for k in BUFFER_NAMES}
+    ref = sampler.infer_spectrogram(lambda s, x, nl: wg.forward(P, s, x.reshape(x.shape[0], -1), nl).reshape(x.shape),
+                                    tab, spec, 300, noise=noise)
+    err = rms(out, ref)
+    print(f"WaveGrad caller noise: rms {err:.3e} (signal rms {rms(ref, 0):.3f})")
+    assert out.shape == ref.shape and np.isfinite(out).all() and err <= 1e-4 * max(1.0, rms(ref, 0))

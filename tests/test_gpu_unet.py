@@ -291,21 +291,28 @@ def test_multilane_graph_replay_equals_row_blocks(torch_cuda, monkeypatch):
     assert err <= 1e-2
 
 
-def test_headline_bf16_vs_fp32_1000_steps(torch_cuda):
+_HEADLINE32 = {}
+
+
+@pytest.mark.parametrize("dtype,gate", [("bfloat16", 5e-3), ("float16", 1e-3)])
+def test_headline_16bit_vs_fp32_1000_steps(torch_cuda, dtype, gate):
     """The benchmarked workload (config #2: T=1000, B=16 x 16448, linear 1e-6..1e-3, condition_in)
-    sampled in bf16 and in fp32 on the HIP path from the same seed: the RMS difference of the
-    denoised outputs is the bf16 drift DESIGN.md §4 quotes (fp32 itself is pinned to the reference
-    at <= 1.2e-7 RMS by the sampling-loop tests)."""
+    sampled in 16 bits and in fp32 on the HIP path from the same seed: the RMS difference of the
+    denoised outputs is the drift DESIGN.md §4 quotes (fp32 itself is pinned to the reference at
+    <= 1.2e-7 RMS by the sampling-loop tests).  fp16 keeps the same bytes and MFMA rate as bf16 and
+    stays inside north_star's 1e-3 bar; bf16 (the configured headline dtype) does not."""
     from sddm_hip.synth import noisy_speech
     N, B, sched = 16448, 16, ("linear", 1000, 1e-6, 1e-3)
     cond = noisy_speech(B, N, seed=1234)
-    out32 = _sample(torch_cuda, make_ctx(N, "float32", sched), cond)
-    out16 = _sample(torch_cuda, make_ctx(N, "bfloat16", sched), cond)
+    if "out" not in _HEADLINE32:
+        _HEADLINE32["out"] = _sample(torch_cuda, make_ctx(N, "float32", sched), cond)
+    out32 = _HEADLINE32["out"]
+    out16 = _sample(torch_cuda, make_ctx(N, dtype, sched), cond)
     assert np.isfinite(out16).all() and np.isfinite(out32).all()
     err = rms(out16, out32)
     rows = [rms(out16[b], out32[b]) for b in range(B)]
-    print(f"T=1000 B=16 bf16 vs fp32: rms {err:.3e}, worst row {max(rows):.3e}, signal rms {rms(out32, 0):.3f}")
-    assert err <= 5e-3
+    print(f"T=1000 B=16 {dtype} vs fp32: rms {err:.3e}, worst row {max(rows):.3e}, signal rms {rms(out32, 0):.3f}")
+    assert err <= gate
 
 
 def test_config5_sampling_b128_lanes(torch_cuda):
