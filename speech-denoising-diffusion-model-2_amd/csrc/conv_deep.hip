@@ -35,15 +35,38 @@ namespace sddm {
 // 16 zero bytes for the halo pixels outside the image (LDS-DMA has no zero fill)
 __device__ __attribute__((aligned(256))) unsigned char g_deep_zero[256];
 
-constexpr int kDeepMaxChunks = 10;
+constexpr int kDeepMaxChunks = 10;   // 64-pixel chunks of a halo plane (640 halo pixels)
+
+// phase stamps: the default set (1 all issued, 2 GroupNorm landed, 3 operand image written, 4 K
+// loop, 5 stored, 6 statistics) or, with -DSDDM_STAMPS_ISSUE, a finer split of the issue phase (1
+// weights issued, 2 staging loads issued, 3 all issued, 4 GroupNorm landed, 5 image written, 6 K loop)
+#ifdef SDDM_STAMPS_ISSUE
+#define DS_W(a) SDDM_STAMP(a, 1)
+#define DS_STG(a) SDDM_STAMP(a, 2)
+#define DS_ISSUED(a) SDDM_STAMP(a, 3)
+#define DS_LANDED(a) SDDM_STAMP(a, 4)
+#define DS_XFORM(a) SDDM_STAMP(a, 5)
+#define DS_KLOOP(a) SDDM_STAMP(a, 6)
+#define DS_STORED(a) do {} while (0)
+#define DS_STATS(a) do {} while (0)
+#else
+#define DS_W(a) do {} while (0)
+#define DS_STG(a) do {} while (0)
+#define DS_ISSUED(a) SDDM_STAMP(a, 1)
+#define DS_LANDED(a) SDDM_STAMP(a, 2)
+#define DS_XFORM(a) SDDM_STAMP(a, 3)
+#define DS_KLOOP(a) SDDM_STAMP(a, 4)
+#define DS_STORED(a) SDDM_STAMP(a, 5)
+#define DS_STATS(a) SDDM_STAMP(a, 6)
+#endif
 
 // timing ablations of the profiling build (SDDM_STAMPS_DBG; results are garbage under any flag):
-// 4 no halo DMA, 32 no weight loads
+// 32 no weight loads
 #ifdef SDDM_STAMPS
 #define SDDM_DEEP_DBG(bit) ((a.dbg & (bit)) != 0)
 #else
 #define SDDM_DEEP_DBG(bit) false
-#endif   // 64-pixel chunks of a halo plane (640 halo pixels)
+#endif
 
 struct DeepGeo { int HR, HC, HP, NCH, PLB, NCR, PLR; };
 
@@ -145,6 +168,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   for (int d = 0; d < D; ++d)
 #pragma unroll
     for (int fc = 0; fc < FC; ++fc) wa[d][fc] = SDDM_DEEP_DBG(32) ? Frag<T>{} : wfrag(min(wv + NW * d, s_last), fc);
+  DS_W(a);
   // (c) identity residual of this thread's epilogue pixels (4 channels each, clamped: unconditional)
   f32x4 idr[EIT];
   {
@@ -205,6 +229,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
       }
     }
   }
+  DS_STG(a);
   // (f) bias + noise embedding of this thread's 4 epilogue channels (after the DMAs: the row
   // depends on the step counter's scalar round trip)
   float bb[4], sshift;
@@ -219,12 +244,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
     const float sbv = a.bias[cs], stv = trow[cs];
     sshift = sbv + (a.temb ? stv : 0.f);
   }
-  SDDM_STAMP(a, 1);
+  DS_ISSUED(a);
 
   // ---------------- 2. GroupNorm finalize ----------------
   if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
   dma_sync();                                            // every wave's DMAs landed, scale / shift visible
-  SDDM_STAMP(a, 2);
+  DS_LANDED(a);
 
   // ---------------- 3. GroupNorm + SiLU in place (zero padding stays zero) ----------------
   if (gn) {
@@ -254,7 +279,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
     }
     lds_sync();
   }
-  SDDM_STAMP(a, 3);
+  DS_XFORM(a);
 
   // ---------------- 4. this wave's K steps ----------------
   int pix_off[FP];
@@ -299,7 +324,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
       }
     }
   }
-  SDDM_STAMP(a, 4);
+  DS_KLOOP(a);
 
   // ---------------- 5. reduce the partial tiles: red[slot][MT][NBP] ----------------
   lds_sync();                                       // every wave is done with the image
@@ -353,7 +378,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
       sn += 1.f;
     }
   }
-  SDDM_STAMP(a, 5);
+  DS_STORED(a);
   if (a.stats) {
     // the lanes of a wave holding the same 4 channels (64 / TPP of them, TPP apart) add by DPP
     // row rotations and two cross-row swizzles, then the NW wave sums through LDS, summed by one
@@ -389,7 +414,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
       dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);
     }
   }
-  SDDM_STAMP(a, 6);
+  DS_STATS(a);
   SDDM_STAMP(a, 7);
 }
 
