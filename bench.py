@@ -150,7 +150,8 @@ def kernel_src_hash():
     return h.hexdigest()[:16]
 
 
-TRAFFIC_FILES = ("r04_hbm_traffic.json", "r04_config5_hbm_traffic.json", "r03_hbm_traffic.json")   # newest first
+TRAFFIC_FILES = ("r05_hbm_traffic.json", "r05_config5_hbm_traffic.json", "r04_hbm_traffic.json",
+                 "r04_config5_hbm_traffic.json")   # newest first
 
 
 def unet_roofline(model, cond, N, B, T, dtype, ms_per_run):

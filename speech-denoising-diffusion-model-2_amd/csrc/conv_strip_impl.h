@@ -111,12 +111,21 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   }
   // weight slabs straight into LDS (LDS-DMA: unit u lands at byte 16 u, co fastest, so every
   // wave-instruction fills 1 KiB of consecutive LDS; no VGPRs, no wait until the first barrier)
-  // NBLK * WPLANES and NBLK * RPLANES are multiples of 64: whole waves, no tail
+  // NBLK * WPLANES and NBLK * RPLANES are multiples of 64: whole waves, no tail.  16-bit weights
+  // come from the chunk-major image ConvArgs::wgt_t ([Cin/32][9][4][Cout][8]), where the NBLK
+  // channels of one plane are one contiguous run: a wave-instruction reads 1 KiB of consecutive
+  // bytes (8 cache lines).  From the per-channel image (fp32) each lane reads another channel's
+  // row, 32-64 lines per instruction, and the LDS-DMA path takes ~3.5x as long (tools/mb_dma.hip).
   for (int u0 = wave * 64; u0 < NBLK * WPLANES; u0 += NT) {
     const int u = u0 + lane;
     const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
-    const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
-    const char* src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
+    const char* src;
+    if constexpr (ES == 2) {
+      src = (const char*)a.wgt_t + ((size_t)pl * a.Cout + n0 + co) * 16;
+    } else {
+      const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
+      src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
+    }
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                      (__attribute__((address_space(3))) void*)(wl + u0 * 16), 16, 0, 0);
   }
@@ -124,7 +133,8 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     for (int u0 = wave * 64; u0 < NBLK * RPLANES; u0 += NT) {
       const int u = u0 + lane;
       const int co = u % NBLK, pl = u / NBLK;
-      const char* src = (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
+      const char* src = ES == 2 ? (const char*)a.res_wgt_t + ((size_t)pl * a.Cout + n0 + co) * 16
+                                : (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(rw + u0 * 16), 16, 0, 0);
     }
@@ -449,6 +459,7 @@ static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size
       (a.res_mode == 2 && (a.RCA + a.RCB) > 128))
     return hipErrorInvalidValue;
   if (a.n_tiles != a.Ho / SR) return hipErrorInvalidValue;
+  if (sizeof(T) == 2 && (!a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))) return hipErrorInvalidValue;
   const dim3 grid = xcd_grid(a.Ho / SR, B, a.Cout / (16 * FC)), blk(MPI * 2);
   if (a.res_mode != 0 && !a.gamma) return hipErrorInvalidValue;   // residual modes are ResnetBlock convs
   if (a.res_mode == 0 && !a.gamma) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0, false>), grid, blk, lds, s, a, SR);
