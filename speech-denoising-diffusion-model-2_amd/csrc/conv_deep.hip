@@ -28,6 +28,7 @@
 // NW = 8 (one block per CU, K split 8 ways) keeps a large K resident for the small late-level
 // grids; NW = 4 (two blocks per CU) overlaps two blocks on the larger grids.
 #include "conv_common.h"
+#include "conv_tile_cfg.h"
 #include "kernels.h"
 
 namespace sddm {
@@ -100,10 +101,42 @@ __host__ __device__ inline DeepLds deep_layout(const DeepGeo& g, int Cin, int RC
 // GroupNorm items per thread: 64 (tile, channel) statistics per group in one round trip
 template <int NW> struct DeepGN { static constexpr int GK = NW == 8 ? 4 : 8; };
 
+// deep kernel shapes (conv_tile_cfg.h ConvShape; cfg = pixels per tile): UNetModified2
+// config_unet.json at 16448 samples with the measured per-layer kernels of configs/conv_tuning.json
+static constexpr ConvShape kDeepShapes[] = {
+    {-1, 0, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},                  // generic (fields unused)
+    {32, 1, 2, 16, 32, 16, 96, 0, 96, 0, 0, 0, 0, 0, 4, 32},             // downs.6
+    {128, 0, 8, 16, 32, 16, 96, 0, 128, 0, 0, 0, 1, 0, 8, 32},           // downs.7.block1
+    {128, 0, 8, 16, 32, 16, 128, 0, 128, 96, 0, 2, 1, 0, 8, 32},         // downs.7.block2
+    {32, 1, 4, 8, 16, 8, 128, 0, 128, 0, 0, 0, 0, 0, 4, 32},             // downs.8
+    {64, 0, 8, 8, 16, 8, 128, 0, 160, 0, 0, 0, 1, 0, 4, 32},             // downs.9.block1
+    {64, 0, 8, 8, 16, 8, 160, 0, 160, 128, 0, 2, 1, 0, 4, 32},           // downs.9.block2
+    {32, 1, 8, 4, 8, 4, 160, 0, 160, 0, 0, 0, 0, 0, 4, 16},              // downs.10
+    {32, 0, 8, 4, 8, 4, 160, 0, 160, 0, 0, 0, 1, 0, 8, 16},              // mid.0.block1
+    {32, 0, 8, 4, 8, 4, 160, 0, 160, 0, 0, 1, 1, 0, 8, 16},              // mid.0.block2
+    {32, 0, 8, 4, 8, 4, 160, 160, 160, 0, 0, 0, 1, 0, 8, 16},            // ups.0.block1
+    {32, 0, 8, 4, 8, 4, 160, 0, 160, 160, 160, 2, 1, 0, 8, 16},          // ups.0.block2
+    {64, 0, 8, 8, 16, 8, 160, 0, 160, 0, 0, 0, 0, 1, 4, 32},             // ups.1
+    {32, 0, 4, 8, 16, 8, 160, 160, 128, 0, 0, 0, 1, 0, 8, 32},           // ups.2.block1
+    {32, 0, 4, 8, 16, 8, 128, 0, 128, 160, 160, 2, 1, 0, 4, 32},         // ups.2.block2
+    {32, 0, 4, 8, 16, 8, 128, 128, 128, 0, 0, 0, 1, 0, 8, 32},           // ups.3.block1
+    {32, 0, 4, 8, 16, 8, 128, 0, 128, 128, 128, 2, 1, 0, 4, 32},         // ups.3.block2
+    {128, 0, 8, 16, 32, 16, 128, 0, 128, 0, 0, 0, 0, 1, 4, 32},          // ups.4
+    {128, 0, 8, 16, 32, 16, 128, 128, 96, 0, 0, 0, 1, 0, 8, 32},         // ups.5.block1
+    {128, 0, 8, 16, 32, 16, 96, 0, 96, 128, 128, 2, 1, 0, 8, 32},        // ups.5.block2
+    {128, 0, 8, 16, 32, 16, 96, 96, 96, 0, 0, 0, 1, 0, 8, 32},           // ups.6.block1
+    {128, 0, 8, 16, 32, 16, 96, 0, 96, 96, 96, 2, 1, 0, 4, 32},          // ups.6.block2
+};
+static constexpr int kNDeepShapes = (int)(sizeof(kDeepShapes) / sizeof(kDeepShapes[0]));
+
 // One output tile (TR x TW pixels of image b, output channels [zb NB, zb NB + NB)).
-template <typename T, bool S2, int MT, int NW, int D, int NB>
+template <typename T, bool S2, int MT, int NW, int D, int NB, int SH>
 __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // layer geometry: compile-time for a specialised shape (SH > 0, kDeepShapes), else the arguments
+  constexpr ConvShape SC = kDeepShapes[SH];
+  constexpr bool CS = SH > 0;
+  SDDM_SHAPE_GEO(SC, CS, S2, a)
   constexpr int NT = 64 * NW;
   constexpr int ES = (int)sizeof(T);
   constexpr int UPP = 2 * ES;          // 16-byte planes per 32-channel chunk
@@ -117,24 +150,24 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;
 
   int tile, b, zb;
-  xcd_block(a.n_tiles, a.Cout / NB, tile, b, zb);
+  xcd_block(gNT, gCout / NB, tile, b, zb);
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n0 = zb * NB;
-  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  const int y0 = ty * a.TR, x0 = tx * a.TW;
-  const int npv = a.TR * a.TW;         // valid pixels (< MT only for images smaller than a tile)
-  const DeepGeo geo = deep_geo(S2, a.TR, a.TW, MT);
+  const int ty = tile / gTX, tx = tile - ty * gTX;
+  const int y0 = ty * gTR, x0 = tx * gTW;
+  const int npv = gTR * gTW;         // valid pixels (< MT only for images smaller than a tile)
+  const DeepGeo geo = deep_geo(S2, gTR, gTW, MT);
   const int HC = geo.HC, PLB = geo.PLB, PLR = geo.PLR;
-  const int Cin = a.CA + a.CB, nck = Cin / 32, npl = Cin / VE, plA = a.CA / VE;
-  const int RC = a.res_mode == 2 ? a.RCA + a.RCB : 0, rck = RC / 32, nplr = RC / VE, plRA = a.RCA / VE;
-  const bool gn = a.gamma != nullptr, ident = a.res_mode == 1;
+  const int Cin = gCA + gCB, nck = Cin / 32, npl = Cin / VE, plA = gCA / VE;
+  const int RC = gRes == 2 ? gRCA + gRCB : 0, rck = RC / 32, nplr = RC / VE, plRA = gRCA / VE;
+  const bool gn = gGN, ident = gRes == 1;
   const DeepLds lay = deep_layout<T, MT, NW, NB>(geo, Cin, RC);
   float* gsc = (float*)(smem + lay.gsc);                 // [2][Cin] GroupNorm scale / shift
   const int res_off = npl * PLB;
-  const int img_in = a.Hi * a.Wi, img_out = a.Ho * a.Wo;
-  const char* srcA = (const char*)a.srcA + (size_t)b * img_in * a.CA * ES;
-  const char* srcB = (const char*)(a.CB ? a.srcB : a.srcA) + (size_t)b * img_in * a.CB * ES;
+  const int img_in = gHi * gWi, img_out = gHo * gWo;
+  const char* srcA = (const char*)a.srcA + (size_t)b * img_in * gCA * ES;
+  const char* srcB = (const char*)(gCB ? a.srcB : a.srcA) + (size_t)b * img_in * gCB * ES;
   const char* zero = (const char*)g_deep_zero;
   // the step counter selecting the noise-embedding row: an unconditional scalar load (a
   // conditional one is waited for at its branch join, in front of every load below)
@@ -149,7 +182,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   // unconditional loads, no wait at a branch join)
   GNLoadT<DeepGN<NW>::GK> gl;
   const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
+  gl.issue(gf, b, gCA, gCB, gn, a.bias);
   // (b) this wave's K steps and the weight fragments of its first D (MFMA-fragment order,
   // ConvArgs::wgt_f: one A fragment = one contiguous 1 KiB (16-bit) / 2 KiB (fp32) run)
   const int ns3 = nck * 9, ns = ns3 + rck;
@@ -172,11 +205,11 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   // (c) identity residual of this thread's epilogue pixels (4 channels each, clamped: unconditional)
   f32x4 idr[EIT];
   {
-    const T* rsrc = (const T*)a.res_src + (size_t)b * img_out * a.Cout + n0 + ec4;
+    const T* rsrc = (const T*)a.res_src + (size_t)b * img_out * gCout + n0 + ec4;
 #pragma unroll
     for (int it = 0; it < EIT; ++it) {
-      const int p = min(it * PPI + tid / TPP, npv - 1), py = p / a.TW, px = p - py * a.TW;
-      const T* rp = ident ? rsrc + ((y0 + py) * a.Wo + (x0 + px)) * a.Cout : (const T*)g_deep_zero;
+      const int p = min(it * PPI + tid / TPP, npv - 1), py = p / gTW, px = p - py * gTW;
+      const T* rp = ident ? rsrc + ((y0 + py) * gWo + (x0 + px)) * gCout : (const T*)g_deep_zero;
       idr[it] = load4<T>(rp);                            // unconditional (zero page without residual)
     }
   }
@@ -198,17 +231,17 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
       bool ok;
       if (S2) {
         iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
-        ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+        ok = iy >= 0 && iy < gHi && ix >= 0 && ix < gWi;
       } else {
         iy = y0 - 1 + hy; ix = x0 - 1 + hx;
-        ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
-        if (a.upsample) { iy >>= 1; ix >>= 1; }
+        ok = iy >= 0 && iy < gHo && ix >= 0 && ix < gWo;
+        if (gUp) { iy >>= 1; ix >>= 1; }
       }
       ok = ok && hp < geo.HP;
       inb |= ok ? 1u << r : 0u;
-      const unsigned pix = ok ? (unsigned)(iy * a.Wi + ix) : 0u;
-      const char* pa = ok ? srcA + pix * (unsigned)(a.CA * ES) : zero;
-      const char* pb = ok ? srcB + pix * (unsigned)(a.CB * ES) - plA * 16 : zero;
+      const unsigned pix = ok ? (unsigned)(iy * gWi + ix) : 0u;
+      const char* pa = ok ? srcA + pix * (unsigned)(gCA * ES) : zero;
+      const char* pb = ok ? srcB + pix * (unsigned)(gCB * ES) - plA * 16 : zero;
       const unsigned step = ok ? 16u : 0u;               // the zero page for every plane outside
       char* dl = smem + r * 1024;
       for (int q = wv; q < npl; q += NW)                 // wave-uniform planes
@@ -217,12 +250,12 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   }
   // (e) the res_conv input at the output pixels (1x1, raw concat)
   if (rck) {
-    const char* rawA = (const char*)a.rawA + (size_t)b * img_out * a.RCA * ES;
-    const char* rawB = (const char*)(a.RCB ? a.rawB : a.rawA) + (size_t)b * img_out * a.RCB * ES;
+    const char* rawA = (const char*)a.rawA + (size_t)b * img_out * gRCA * ES;
+    const char* rawB = (const char*)(gRCB ? a.rawB : a.rawA) + (size_t)b * img_out * gRCB * ES;
     for (int r = 0; r < geo.NCR; ++r) {
-      const int p = r * 64 + lane, py = p / a.TW, px = p - py * a.TW;
-      const int pix = p < npv ? (y0 + py) * a.Wo + (x0 + px) : -1;
-      const unsigned oa = (unsigned)pix * (unsigned)(a.RCA * ES), ob = (unsigned)pix * (unsigned)(a.RCB * ES);
+      const int p = r * 64 + lane, py = p / gTW, px = p - py * gTW;
+      const int pix = p < npv ? (y0 + py) * gWo + (x0 + px) : -1;
+      const unsigned oa = (unsigned)pix * (unsigned)(gRCA * ES), ob = (unsigned)pix * (unsigned)(gRCB * ES);
       for (int q = wv; q < nplr; q += NW) {
         const char* src = q < plRA ? rawA + oa + q * 16 : rawB + ob + (q - plRA) * 16;
         dma(pix >= 0 ? src : zero, smem + res_off + q * PLR + r * 1024);
@@ -247,7 +280,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   DS_ISSUED(a);
 
   // ---------------- 2. GroupNorm finalize ----------------
-  if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
+  if (gn) gl.finish(gf, b, gCA, gCB, gsc, gsc + Cin);
   dma_sync();                                            // every wave's DMAs landed, scale / shift visible
   DS_LANDED(a);
 
@@ -287,7 +320,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   for (int fp = 0; fp < FP; ++fp) {
     int p = fp * 16 + (lane & 15);
     if (p >= npv) p = 0;
-    const int py = p / a.TW, px = p - py * a.TW;
+    const int py = p / gTW, px = p - py * gTW;
     pix_off[fp] = S2 ? ((2 * py) * HC + 2 * px) * 16 : (py * HC + px) * 16;
   }
   f32x4 acc[FP][FC];
@@ -357,19 +390,19 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   float sn = 0.f, s1[4], s2[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) { s1[i] = 0.f; s2[i] = 0.f; }
-  T* out = (T*)a.out + (size_t)b * img_out * a.Cout + n0 + ec4;
+  T* out = (T*)a.out + (size_t)b * img_out * gCout + n0 + ec4;
 #pragma unroll
   for (int it = 0; it < EIT; ++it) {
     const int p = it * PPI + tid / TPP;
     if (p < npv) {
-      const int py = p / a.TW, px = p - py * a.TW;
+      const int py = p / gTW, px = p - py * gTW;
       f32x4 s = *(const f32x4*)(red + p * NBP + ec4);
 #pragma unroll
       for (int w = 1; w < SLOTS; ++w) s += *(const f32x4*)(red + (w * MT + p) * NBP + ec4);
       float d[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) d[i] = s[i] + idr[it][i];
-      store4<T>(out + ((y0 + py) * a.Wo + (x0 + px)) * a.Cout, d[0] + bb[0], d[1] + bb[1], d[2] + bb[2], d[3] + bb[3]);
+      store4<T>(out + ((y0 + py) * gWo + (x0 + px)) * gCout, d[0] + bb[0], d[1] + bb[1], d[2] + bb[2], d[3] + bb[3]);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {                    // sums about the shift bb (the same for
         s1[i] += d[i];                                 // every thread of a channel: they add)
@@ -409,7 +442,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
         const float* e = xs + (r * NB + tid) * 3;
         n += e[0]; u1 += e[1]; u2 += e[2];
       }
-      float* dst = a.stats + (((size_t)b * a.n_tiles + tile) * a.Cout + n0 + tid) * 2;
+      float* dst = a.stats + (((size_t)b * gNT + tile) * gCout + n0 + tid) * 2;
       dst[0] = (sshift + u1 / n) * n;
       dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);
     }
@@ -426,7 +459,7 @@ static int deep_ring(int steps_per_wave) {
   return 12;
 }
 
-template <typename T, bool S2, int MT, int NW, int NB>
+template <typename T, bool S2, int MT, int NW, int NB, int SH = 0>
 static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   const int Cin = a.CA + a.CB, RC = a.res_mode == 2 ? a.RCA + a.RCB : 0;
   const int nck = Cin / 32, rck = RC / 32;
@@ -444,10 +477,15 @@ static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   const int D = deep_ring<T, MT, NW>((nck * 9 + rck + NW - 1) / NW);
 #define SDDM_RING(DV)                                                                         \
   if (D == DV) {                                                                              \
-    hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT, NW, DV, NB>), grid, blk, lay.total, s, a); \
+    hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT, NW, DV, NB, SH>), grid, blk, lay.total, s, a); \
     return hipGetLastError();                                                                 \
   }
-  if constexpr (sizeof(T) == 4) {
+  if constexpr (SH > 0) {                                 // one ring depth per specialised shape
+    constexpr ConvShape c = kDeepShapes[SH];
+    constexpr int spw = (((c.CA + c.CB) / 32) * 9 + (c.res == 2 ? (c.RCA + c.RCB) / 32 : 0) + NW - 1) / NW;
+    constexpr int DS = (NW == 4 || MT >= 128 || spw <= 8) ? 8 : 12;
+    SDDM_RING(DS)
+  } else if constexpr (sizeof(T) == 4) {
     SDDM_RING(4)
   } else if constexpr (NW == 4 || MT >= 128) {
     SDDM_RING(8)
@@ -458,9 +496,27 @@ static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   return hipErrorInvalidValue;
 }
 
+// the specialised shapes SH = 1 .. kNDeepShapes-1 (16-bit storage only) matching the launch
+template <typename T, int SH>
+static bool deep_shape_go(int mt, int nw, int nb, bool s2, const ConvArgs& a, int B, hipStream_t s, hipError_t& e) {
+  if constexpr (SH >= kNDeepShapes || sizeof(T) == 4) {
+    return false;
+  } else {
+    constexpr ConvShape c = kDeepShapes[SH];
+    if (c.cfg == mt && c.nw == nw && c.nb == nb && conv_shape_geo_matches(c, s2, a)) {
+      e = deep_go<T, c.s2 != 0, c.cfg, c.nw, c.nb, SH>(a, B, s, nullptr);
+      return true;
+    }
+    return deep_shape_go<T, SH + 1>(mt, nw, nb, s2, a, B, s, e);
+  }
+}
+
 // nb: output channels per block (32, or 16 for twice the blocks with half the weight bytes each)
 template <typename T>
 static hipError_t deep_dispatch(int mt, int nw, int nb, bool s2, const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
+  static const bool generic = std::getenv("SDDM_NO_DEEP_SHAPES") != nullptr;   // A/B runs
+  hipError_t e;
+  if (!lo && !generic && deep_shape_go<T, 1>(mt, nw, nb, s2, a, B, s, e)) return e;
 #define SDDM_DEEP(S2V, MTV, NWV, NBV) \
   if (s2 == S2V && mt == MTV && nw == NWV && nb == NBV) return deep_go<T, S2V, MTV, NWV, NBV>(a, B, s, lo);
   SDDM_DEEP(false, 32, 4, 32) SDDM_DEEP(false, 64, 4, 32) SDDM_DEEP(false, 128, 4, 32)

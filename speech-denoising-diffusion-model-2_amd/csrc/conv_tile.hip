@@ -32,7 +32,7 @@
 
 namespace sddm {
 
-template <typename T, bool S2, int WPX, int WCO, int FP, int FC, int MAXU>
+template <typename T, bool S2, int WPX, int WCO, int FP, int FC, int MAXU, int SH>
 __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   constexpr int NWV = WPX * WCO, NT = 64 * NWV;
   constexpr int MT = WPX * FP * 16, NB = WCO * FC * 16;
@@ -40,38 +40,42 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   static_assert(sizeof(T) == 2, "conv_tile is the 16-bit path");
   typedef T vec4 __attribute__((ext_vector_type(4)));
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // layer geometry: compile-time for a specialised shape (SH > 0, kTileShapes), else the arguments
+  constexpr ConvShape SC = kTileShapes[SH];
+  constexpr bool CS = SH > 0;
+  SDDM_SHAPE_GEO(SC, CS, S2, a)
 
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4, c16 = lane & 15, q = lane & 3;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wp = wv % WPX, wc = wv / WPX;
   int tile, b, zb;
-  xcd_block<SDDM_XCD_ZIN != 0>(a.n_tiles, a.Cout / NB, tile, b, zb);
+  xcd_block<SDDM_XCD_ZIN != 0>(gNT, gCout / NB, tile, b, zb);
   const int n0 = zb * NB;
-  const int ty = tile / a.tiles_x, tx = tile - ty * a.tiles_x;
-  const int y0 = ty * a.TR, x0 = tx * a.TW;
-  const int npv = a.TR * a.TW;                             // valid pixels (< MT: image smaller than a tile)
-  const int Cin = a.CA + a.CB, nck = Cin / 32, ckA = a.CA / 32;
-  const int RC = a.RCA + a.RCB, rck = a.res_mode == 2 ? RC / 32 : 0, rckA = a.RCA / 32;
+  const int ty = tile / gTX, tx = tile - ty * gTX;
+  const int y0 = ty * gTR, x0 = tx * gTW;
+  const int npv = gTR * gTW;                             // valid pixels (< MT: image smaller than a tile)
+  const int Cin = gCA + gCB, nck = Cin / 32, ckA = gCA / 32;
+  const int RC = gRCA + gRCB, rck = gRes == 2 ? RC / 32 : 0, rckA = gRCA / 32;
   const int nk = nck + rck;
-  const bool gn = a.gamma != nullptr, ident = a.res_mode == 1;
-  const TileGeo geo = tile_geo(S2, a.TR, a.TW, MT, rck > 0);
+  const bool gn = gGN, ident = gRes == 1;
+  const TileGeo geo = tile_geo(S2, gTR, gTW, MT, rck > 0);
   const int HC = geo.HC, HE = geo.HE, PLB = geo.PLB;
   const int nbuf = nk > 1 ? 2 : 1;                         // double buffers only when K streams
   char* IB = smem;                                         // [nbuf][4 planes][PLB] operand images
   char* WB = IB + nbuf * geo.ibb;                          // [nbuf][WCH]           weight chunks
   float* gsc = (float*)(WB + nbuf * WCH);                  // [2][Cin]              GroupNorm scale / shift
-  const float rHC = 1.0f / (float)HC, rTW = 1.0f / (float)a.TW;
-  const int img_in = a.Hi * a.Wi, img_out = a.Ho * a.Wo;
-  const T* srcA = (const T*)a.srcA + (size_t)b * img_in * a.CA;
-  const T* srcB = a.CB ? (const T*)a.srcB + (size_t)b * img_in * a.CB : srcA;
-  const T* rawA = rck ? (const T*)a.rawA + (size_t)b * img_out * a.RCA : srcA;
-  const T* rawB = (rck && a.RCB) ? (const T*)a.rawB + (size_t)b * img_out * a.RCB : rawA;
+  const float rHC = 1.0f / (float)HC, rTW = 1.0f / (float)gTW;
+  const int img_in = gHi * gWi, img_out = gHo * gWo;
+  const T* srcA = (const T*)a.srcA + (size_t)b * img_in * gCA;
+  const T* srcB = gCB ? (const T*)a.srcB + (size_t)b * img_in * gCB : srcA;
+  const T* rawA = rck ? (const T*)a.rawA + (size_t)b * img_out * gRCA : srcA;
+  const T* rawB = (rck && gRCB) ? (const T*)a.rawB + (size_t)b * img_out * gRCB : rawA;
   SDDM_STAMP(a, 0);
 
   // ---------------- prologue: every independent load before anything waits ----------------
   GNLoad gl;
   const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
+  gl.issue(gf, b, gCA, gCB, gn, a.bias);
   const int t_now = a.t_dev ? *a.t_dev : 0;
   const float* trow = a.temb ? a.temb + (size_t)(a.temb_per_b ? b : t_now) * a.temb_ld : a.bias;
   const int cw0 = wc * FC * 16, pw0 = wp * FP * 16;
@@ -99,14 +103,14 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     pok[fp] = p < npv;
     if (!pok[fp]) p = 0;
     ppy[fp] = fdivi(p, rTW);
-    ppx[fp] = p - ppy[fp] * a.TW;
+    ppx[fp] = p - ppy[fp] * gTW;
   }
   vec4 r1[FP][FC];                                         // identity residual (res_conv = Identity)
   {
-    const T* rs = ident ? (const T*)a.res_src + (size_t)b * img_out * a.Cout : srcA;
+    const T* rs = ident ? (const T*)a.res_src + (size_t)b * img_out * gCout : srcA;
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp) {
-      const int po = ident ? ((y0 + ppy[fp]) * a.Wo + (x0 + ppx[fp])) * a.Cout : 0;
+      const int po = ident ? ((y0 + ppy[fp]) * gWo + (x0 + ppx[fp])) * gCout : 0;
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) r1[fp][fc] = *(const vec4*)(rs + po + (ident ? n0 + cw0 + fc * 16 + 4 * g : 0));
     }
@@ -123,15 +127,15 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     bool ok;
     if (S2) {
       iy = 2 * y0 - 1 + hy; ix = 2 * x0 - 1 + hx;
-      ok = iy >= 0 && iy < a.Hi && ix >= 0 && ix < a.Wi;
+      ok = iy >= 0 && iy < gHi && ix >= 0 && ix < gWi;
       slot = hy * HC + ((hx & 1) ? HE + (hx >> 1) : (hx >> 1));
     } else {
       iy = y0 - 1 + hy; ix = x0 - 1 + hx;
-      ok = iy >= 0 && iy < a.Ho && ix >= 0 && ix < a.Wo;
-      if (a.upsample) { iy >>= 1; ix >>= 1; }
+      ok = iy >= 0 && iy < gHo && ix >= 0 && ix < gWo;
+      if (gUp) { iy >>= 1; ix >>= 1; }
       slot = s;
     }
-    spx[j] = ok ? iy * a.Wi + ix : -1;
+    spx[j] = ok ? iy * gWi + ix : -1;
     sof[j] = u < geo.nu3 ? q * PLB + ((slot ^ (q << 1)) << 4) : -1;
   }
 
@@ -141,19 +145,19 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     if (k < nck) {
       const bool fa = k < ckA;
       const T* base = (fa ? srcA + k * 32 : srcB + (k - ckA) * 32) + q * 8;
-      const int cs = fa ? a.CA : a.CB;
+      const int cs = fa ? gCA : gCB;
 #pragma unroll
       for (int j = 0; j < MAXU; ++j) rr[j] = *(const f32x4*)(base + (spx[j] < 0 ? 0 : spx[j] * cs));
     } else {                                               // res_conv chunk: raw input at the output pixels
       const int r = k - nck;
       const bool fa = r < rckA;
       const T* base = (fa ? rawA + r * 32 : rawB + (r - rckA) * 32) + q * 8;
-      const int cs = fa ? a.RCA : a.RCB;
+      const int cs = fa ? gRCA : gRCB;
 #pragma unroll
       for (int j = 0; j < MAXU; ++j) {
         const int p = (tid + j * NT) >> 2;
-        const int py = fdivi(p, rTW), px = p - py * a.TW;
-        rr[j] = *(const f32x4*)(base + (p < npv ? ((y0 + py) * a.Wo + (x0 + px)) * cs : 0));
+        const int py = fdivi(p, rTW), px = p - py * gTW;
+        rr[j] = *(const f32x4*)(base + (p < npv ? ((y0 + py) * gWo + (x0 + px)) * cs : 0));
       }
     }
   };
@@ -162,11 +166,11 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     char* dst = WB + buf * WCH;
     const bool res = k >= nck;
     const int nw = (res ? 4 : 36) * NB;
-    const char* ws = res ? (const char*)a.res_wgt_t + (size_t)(k - nck) * 4 * a.Cout * 16
-                         : (const char*)a.wgt_t + (size_t)k * 36 * a.Cout * 16;
+    const char* ws = res ? (const char*)a.res_wgt_t + (size_t)(k - nck) * 4 * gCout * 16
+                         : (const char*)a.wgt_t + (size_t)k * 36 * gCout * 16;
     for (int u0 = wv * 64; u0 < nw; u0 += NT) {
       const int u = u0 + lane, r = u / NB, co = u - r * NB;
-      glds16(ws + ((size_t)r * a.Cout + n0 + co) * 16, dst + u0 * 16);
+      glds16(ws + ((size_t)r * gCout + n0 + co) * 16, dst + u0 * 16);
     }
   };
   // chunk k: registers -> IB[buf] with zero padding and GroupNorm + SiLU (3x3 chunks of a Block)
@@ -249,7 +253,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
 
   load_raw(0);
   issue_w(0, 0);
-  if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + Cin);
+  if (gn) gl.finish(gf, b, gCA, gCB, gsc, gsc + Cin);
   SDDM_STAMP(a, 1);
   __syncthreads();                                         // gsc visible
   transform(0, 0);
@@ -275,7 +279,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   SDDM_STAMP(a, 4);
 
   // ---------------- epilogue ----------------
-  T* out = (T*)a.out + (size_t)b * img_out * a.Cout;
+  T* out = (T*)a.out + (size_t)b * img_out * gCout;
   float s1[FC][4], s2[FC][4], nl = 0.f;
 #pragma unroll
   for (int fc = 0; fc < FC; ++fc)
@@ -285,7 +289,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   for (int fp = 0; fp < FP; ++fp) {
     if (!pok[fp]) continue;
     nl += 1.f;
-    const int po = ((y0 + ppy[fp]) * a.Wo + (x0 + ppx[fp])) * a.Cout;
+    const int po = ((y0 + ppy[fp]) * gWo + (x0 + ppx[fp])) * gCout;
 #pragma unroll
     for (int fc = 0; fc < FC; ++fc) {
       const int co = n0 + cw0 + fc * 16 + 4 * g;
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
       }
       const int co = tid;
       const float mean = sshift + t1 / n;
-      float* dst = a.stats + (((size_t)b * a.n_tiles + tile) * a.Cout + n0 + co) * 2;
+      float* dst = a.stats + (((size_t)b * gNT + tile) * gCout + n0 + co) * 2;
       dst[0] = mean * n;
       dst[1] = fmaxf(t2 - t1 * t1 / n, 0.f);
     }
@@ -346,7 +350,7 @@ static size_t tile_lds_cfg(bool s2, const ConvArgs& a) {
   return (size_t)tile_lds(g, NB, a.CA + a.CB, nk > 1 ? 2 : 1);
 }
 
-template <typename T, bool S2, int I>
+template <typename T, bool S2, int I, int SH = 0>
 static hipError_t tile_go(const ConvArgs& a, int B, hipStream_t s) {
   constexpr TileCfgX c = kTileCfgs[I];
   constexpr int MT = c.wpx * c.fp * 16, NB = c.wco * c.fc * 16;
@@ -354,13 +358,30 @@ static hipError_t tile_go(const ConvArgs& a, int B, hipStream_t s) {
   if (a.TR * a.TW > MT || a.Cout % NB || (a.CA + a.CB) % 32 || a.CA % 32 || (a.RCA + a.RCB) % 32 || a.RCA % 32 ||
       lds > kLdsBytes || !a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL((conv_tile_kernel<T, S2, c.wpx, c.wco, c.fp, c.fc, S2 ? c.maxu_s2 : c.maxu>),
+  hipLaunchKernelGGL((conv_tile_kernel<T, S2, c.wpx, c.wco, c.fp, c.fc, S2 ? c.maxu_s2 : c.maxu, SH>),
                      xcd_grid(a.n_tiles, B, a.Cout / NB), dim3(64 * c.wpx * c.wco), lds, s, a);
   return hipGetLastError();
 }
 
+// the specialised shapes SH = 1 .. kNTileShapes-1 whose configuration, stride and geometry match
+template <typename T, bool S2, int SH>
+static bool tile_shape_go(int cfg, const ConvArgs& a, int B, hipStream_t s, hipError_t& e) {
+  if constexpr (SH >= kNTileShapes) {
+    return false;
+  } else {
+    constexpr ConvShape c = kTileShapes[SH];
+    if constexpr (c.s2 == (S2 ? 1 : 0)) {
+      if (c.cfg == cfg && conv_shape_geo_matches(c, S2, a)) { e = tile_go<T, S2, c.cfg, SH>(a, B, s); return true; }
+    }
+    return tile_shape_go<T, S2, SH + 1>(cfg, a, B, s, e);
+  }
+}
+
 template <typename T, bool S2>
 static hipError_t tile_dispatch(int cfg, const ConvArgs& a, int B, hipStream_t s) {
+  static const bool generic = std::getenv("SDDM_NO_TILE_SHAPES") != nullptr;   // A/B runs
+  hipError_t e;
+  if (!generic && tile_shape_go<T, S2, 1>(cfg, a, B, s, e)) return e;
   switch (cfg) {
 #define SDDM_TILE(I) \
   case I: return tile_go<T, S2, I>(a, B, s);
