@@ -42,12 +42,45 @@
 #endif
 
 #include "conv_common.h"
+#include "conv_tile_cfg.h"
 #include "kernels.h"
 
 namespace sddm {
 
-template <typename T, int FC, int W, int CIN, int MPI, int RES, bool GN>
-__global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR) {
+// strip kernel shapes (conv_tile_cfg.h ConvShape; cfg = output channels per block, TR = nb =
+// strip rows, TW = W, nw = pixels per iteration): UNetModified2 config_unet.json at 16448 samples
+// with the kernels of configs/conv_tuning.json
+static constexpr ConvShape kStripShapes[] = {
+    {-1, 0, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},   // generic (fields unused)
+    {32, 0, 16, 128, 256, 128, 32, 0, 32, 0, 0, 0, 1, 0, 256, 16},      // downs.1.block1
+    {32, 0, 16, 128, 256, 128, 32, 0, 32, 0, 0, 1, 1, 0, 256, 16},      // downs.1.block2
+    {64, 0, 8, 64, 128, 64, 32, 0, 64, 0, 0, 0, 1, 0, 256, 8},          // downs.3.block1
+    {32, 0, 16, 64, 128, 64, 64, 0, 64, 32, 0, 2, 1, 0, 256, 16},       // downs.3.block2
+    {32, 0, 16, 64, 128, 64, 64, 0, 64, 0, 0, 0, 0, 1, 256, 16},        // ups.10 (Upsample)
+    {32, 0, 8, 64, 128, 64, 32, 0, 32, 64, 64, 2, 1, 0, 256, 8},        // ups.11.block2
+    {32, 0, 8, 64, 128, 64, 32, 32, 32, 0, 0, 0, 1, 0, 256, 8},         // ups.12.block1
+    {32, 0, 8, 64, 128, 64, 32, 0, 32, 32, 32, 2, 1, 0, 256, 8},        // ups.12.block2
+    {32, 0, 16, 128, 256, 128, 32, 0, 32, 0, 0, 0, 0, 1, 256, 16},      // ups.13 (Upsample)
+    {32, 0, 16, 128, 256, 128, 32, 32, 32, 0, 0, 0, 1, 0, 256, 16},     // ups.14.block1
+    {32, 0, 16, 128, 256, 128, 32, 0, 32, 32, 32, 2, 1, 0, 256, 16},    // ups.14.block2
+};
+static constexpr int kNStripShapes = (int)(sizeof(kStripShapes) / sizeof(kStripShapes[0]));
+
+__host__ inline bool strip_shape_matches(const ConvShape& c, int nblk, int mpi, int SR, const ConvArgs& a) {
+  return c.cfg == nblk && c.nw == mpi && c.nb == SR && c.Ho == a.Ho && c.Wo == a.Wo && c.CA == a.CA && c.CB == a.CB &&
+         c.Cout == a.Cout && c.RCA == a.RCA && c.RCB == a.RCB && c.res == a.res_mode &&
+         c.gn == (a.gamma != nullptr ? 1 : 0) && c.up == (a.upsample ? 1 : 0) && a.n_tiles == c.Ho / SR &&
+         a.Hi == (c.up ? c.Ho / 2 : c.Ho) && a.Wi == (c.up ? c.Wo / 2 : c.Wo);
+}
+
+template <typename T, int FC, int W, int CIN, int MPI, int RES, bool GN, int SH>
+__global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR_) {
+  // layer geometry: compile-time for a specialised shape (SH > 0), else the arguments
+  constexpr ConvShape SC = kStripShapes[SH];
+  constexpr bool CS = SH > 0;
+  SDDM_SHAPE_GEO(SC, CS, false, a)
+  const int SR = CS ? SC.nb : SR_;
+  (void)gTR; (void)gTW; (void)gTX; (void)gRes; (void)gGN; (void)gWo;
   constexpr int NT = MPI * 2;                     // threads: one wave per 32 pixels of an iteration
   constexpr int NWV = NT / 64;
   constexpr int ES = (int)sizeof(T);
@@ -73,10 +106,10 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   int strip, b, zb;
-  xcd_block<SDDM_XCD_ZIN != 0>(a.n_tiles, a.Cout / NBLK, strip, b, zb);
+  xcd_block<SDDM_XCD_ZIN != 0>(gNT, gCout / NBLK, strip, b, zb);
   const int n0 = zb * NBLK;
-  const int H = a.Ho;
-  const int RC = a.RCA + a.RCB;
+  const int H = gHo;
+  const int RC = gRCA + gRCB;
   const int rck = RES == 2 ? RC / 32 : 0;
   constexpr bool gn = GN;                         // GroupNorm + SiLU on the input (a Block conv)
 
@@ -93,10 +126,10 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
   // ---------------- prologue: every independent load issued before anything waits ----------------
   GNLoad gl;
   const GNFuse gf{a.gstA, a.gtilesA, a.gntileA, a.gstB, a.gtilesB, a.gntileB, a.gamma, a.beta, a.groups, a.eps};
-  gl.issue(gf, b, a.CA, a.CB, gn, a.bias);
+  gl.issue(gf, b, gCA, gCB, gn, a.bias);
   // initial ring rows y0-1 .. y0+TR (raw), clamped addresses, zero rows outside the image later
-  const T* srcAb = (const T*)a.srcA + (size_t)b * a.Hi * a.Wi * a.CA;
-  const T* srcBb = a.CB ? (const T*)a.srcB + (size_t)b * a.Hi * a.Wi * a.CB : srcAb;
+  const T* srcAb = (const T*)a.srcA + (size_t)b * gHi * gWi * gCA;
+  const T* srcBb = gCB ? (const T*)a.srcB + (size_t)b * gHi * gWi * gCB : srcAb;
   f32x4 ini[IU];
 #pragma unroll
   for (int k = 0; k < IU; ++k) {
@@ -104,10 +137,10 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     const int grp = u >> 6, j = u & 63;
     const int pix = grp * PB + (j % PB), q = j / PB, r = pix / W, x = pix % W;
     const int ry = min(max(y0 - 1 + r, 0), H - 1);
-    const int sy = a.upsample ? ry >> 1 : ry, sx = a.upsample ? x >> 1 : x;
+    const int sy = gUp ? ry >> 1 : ry, sx = gUp ? x >> 1 : x;
     const int c0 = q * VE;
-    const bool fa = c0 < a.CA;
-    ini[k] = *(const f32x4*)((fa ? srcAb : srcBb) + ((size_t)sy * a.Wi + sx) * (fa ? a.CA : a.CB) + (fa ? c0 : c0 - a.CA));
+    const bool fa = c0 < gCA;
+    ini[k] = *(const f32x4*)((fa ? srcAb : srcBb) + ((size_t)sy * gWi + sx) * (fa ? gCA : gCB) + (fa ? c0 : c0 - gCA));
   }
   // weight slabs straight into LDS (LDS-DMA: unit u lands at byte 16 u, co fastest, so every
   // wave-instruction fills 1 KiB of consecutive LDS; no VGPRs, no wait until the first barrier)
@@ -121,7 +154,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
     const char* src;
     if constexpr (ES == 2) {
-      src = (const char*)a.wgt_t + ((size_t)pl * a.Cout + n0 + co) * 16;
+      src = (const char*)a.wgt_t + ((size_t)pl * gCout + n0 + co) * 16;
     } else {
       const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
       src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
@@ -133,7 +166,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     for (int u0 = wave * 64; u0 < NBLK * RPLANES; u0 += NT) {
       const int u = u0 + lane;
       const int co = u % NBLK, pl = u / NBLK;
-      const char* src = ES == 2 ? (const char*)a.res_wgt_t + ((size_t)pl * a.Cout + n0 + co) * 16
+      const char* src = ES == 2 ? (const char*)a.res_wgt_t + ((size_t)pl * gCout + n0 + co) * 16
                                 : (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                        (__attribute__((address_space(3))) void*)(rw + u0 * 16), 16, 0, 0);
@@ -143,7 +176,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     const int side = u & 1, pl = u >> 1;
     *(f32x4*)(ring + pl * PL + (side ? (W + 1) : 0) * 16) = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  if (gn) gl.finish(gf, b, a.CA, a.CB, gsc, gsc + CIN);
+  if (gn) gl.finish(gf, b, gCA, gCB, gsc, gsc + CIN);
   __syncthreads();                                         // gsc ready
   // bias + noise embedding of this lane's epilogue channels (Cout % NBLK == 0: no clamping)
   const int t_now = a.t_dev ? *a.t_dev : 0;
@@ -206,17 +239,17 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     loff[k] = q * PL + (x + 1) * 16;
     cq[k] = q * VE;
     const int c0 = q * VE;
-    const int sx = a.upsample ? (x >> 1) : x;
-    const bool fa = c0 < a.CA;
-    rsrc_[k] = fa ? (const char*)(srcAb + sx * a.CA + c0) : (const char*)(srcBb + sx * a.CB + (c0 - a.CA));
-    rstr[k] = (unsigned)(a.Wi * (fa ? a.CA : a.CB) * ES);
+    const int sx = gUp ? (x >> 1) : x;
+    const bool fa = c0 < gCA;
+    rsrc_[k] = fa ? (const char*)(srcAb + sx * gCA + c0) : (const char*)(srcBb + sx * gCB + (c0 - gCA));
+    rstr[k] = (unsigned)(gWi * (fa ? gCA : gCB) * ES);
   }
   // rows of row group j (clamped: the groups past the strip end load valid rows nobody reads)
   auto issue_rows = [&](f32x4 (&dst)[UPT], int j) {
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
       const int ry = min(y0 + j * TR + 1 + pr[k], H - 1);
-      const int sy = a.upsample ? (ry >> 1) : ry;
+      const int sy = gUp ? (ry >> 1) : ry;
       dst[k] = *(const f32x4*)(rsrc_[k] + (unsigned)__umul24((unsigned)sy, rstr[k]));
     }
   };
@@ -238,20 +271,20 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
       *(f32x4*)(ring + (int)__umul24(sl, SLOT) + loff[k]) = tv[k];
     }
   };
-  T* outb = (T*)a.out + (size_t)b * H * W * a.Cout;
+  T* outb = (T*)a.out + (size_t)b * H * W * gCout;
   // residual inputs of iteration it (issued one iteration ahead; rows clamped into the image)
-  const T* resb = RES == 1 ? (const T*)a.res_src + (size_t)b * H * W * a.Cout : outb;
+  const T* resb = RES == 1 ? (const T*)a.res_src + (size_t)b * H * W * gCout : outb;
   auto issue_res1 = [&](vec4 (&dst)[FP][FC], int it) {
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp) {
       const int yy = min(y0 + it * TR, H - TR) + prow[fp];
-      const unsigned po = (unsigned)(yy * W * a.Cout) + __umul24((unsigned)pcol[fp], (unsigned)a.Cout) + n0 + 4 * g;
+      const unsigned po = (unsigned)(yy * W * gCout) + __umul24((unsigned)pcol[fp], (unsigned)gCout) + n0 + 4 * g;
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) dst[fp][fc] = *(const vec4*)((const char*)resb + (po * ES + fc * 16 * ES));
     }
   };
-  const T* rawAb = RES == 2 ? (const T*)a.rawA + (size_t)b * H * W * a.RCA : outb;
-  const T* rawBb = (RES == 2 && a.RCB) ? (const T*)a.rawB + (size_t)b * H * W * a.RCB : rawAb;
+  const T* rawAb = RES == 2 ? (const T*)a.rawA + (size_t)b * H * W * gRCA : outb;
+  const T* rawBb = (RES == 2 && gRCB) ? (const T*)a.rawB + (size_t)b * H * W * gRCB : rawAb;
   auto issue_res2 = [&](Frag<T> (&dst)[RCKM][FP], int it) {
 #pragma unroll
     for (int ck = 0; ck < RCKM; ++ck)
@@ -260,7 +293,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         const int yy = min(y0 + it * TR, H - TR) + prow[fp];
         const int c0 = min(ck, rck - 1) * 32 + g * 8;
         const int pix = yy * W + pcol[fp];
-        const T* sp = c0 < a.RCA ? rawAb + ((int)__umul24(pix, a.RCA) + c0) : rawBb + ((int)__umul24(pix, a.RCB) + (c0 - a.RCA));
+        const T* sp = c0 < gRCA ? rawAb + ((int)__umul24(pix, gRCA) + c0) : rawBb + ((int)__umul24(pix, gRCB) + (c0 - gRCA));
         dst[ck][fp] = load_frag<T>((const char*)sp);
       }
   };
@@ -364,7 +397,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
     // ---- epilogue: bias + embedding + residual, store, statistics ----
 #pragma unroll
     for (int fp = 0; fp < FP; ++fp) {
-      const unsigned po = (unsigned)((y + prow[fp]) * W * a.Cout) + __umul24((unsigned)pcol[fp], (unsigned)a.Cout);
+      const unsigned po = (unsigned)((y + prow[fp]) * W * gCout) + __umul24((unsigned)pcol[fp], (unsigned)gCout);
 #pragma unroll
       for (int fc = 0; fc < FC; ++fc) {
         const unsigned co = n0 + fc * 16 + 4 * g;
@@ -431,7 +464,7 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR)
         const float* rr = red + (w * NBLK + tid) * 3;
         n += rr[0]; u1 += rr[1]; u2 += rr[2];
       }
-      float* dst = a.stats + (((size_t)b * a.n_tiles + strip) * a.Cout + n0 + tid) * 2;
+      float* dst = a.stats + (((size_t)b * gNT + strip) * gCout + n0 + tid) * 2;
       dst[0] = (sshift + u1 / n) * n;
       dst[1] = fmaxf(u2 - u1 * u1 / n, 0.f);
     }
@@ -450,7 +483,7 @@ static size_t strip_lds(const ConvArgs& a) {
   return n;
 }
 
-template <typename T, int FC, int W, int CIN, int MPI>
+template <typename T, int FC, int W, int CIN, int MPI, int SH = 0>
 static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size_t* lo) {
   const size_t lds = strip_lds<T, FC, W, CIN, MPI>(a);
   if (lo) { *lo = lds; return hipSuccess; }
@@ -462,16 +495,37 @@ static hipError_t strip_go(const ConvArgs& a, int SR, int B, hipStream_t s, size
   if (sizeof(T) == 2 && (!a.wgt_t || (a.res_mode == 2 && !a.res_wgt_t))) return hipErrorInvalidValue;
   const dim3 grid = xcd_grid(a.Ho / SR, B, a.Cout / (16 * FC)), blk(MPI * 2);
   if (a.res_mode != 0 && !a.gamma) return hipErrorInvalidValue;   // residual modes are ResnetBlock convs
-  if (a.res_mode == 0 && !a.gamma) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0, false>), grid, blk, lds, s, a, SR);
-  else if (a.res_mode == 0) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0, true>), grid, blk, lds, s, a, SR);
-  else if (a.res_mode == 1) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 1, true>), grid, blk, lds, s, a, SR);
-  else hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 2, true>), grid, blk, lds, s, a, SR);
+  if constexpr (SH > 0) {                                 // residual mode and GroupNorm from the shape
+    constexpr ConvShape c = kStripShapes[SH];
+    hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, c.res, c.gn != 0, SH>), grid, blk, lds, s, a, SR);
+  } else if (a.res_mode == 0 && !a.gamma) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0, false, 0>), grid, blk, lds, s, a, SR);
+  else if (a.res_mode == 0) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 0, true, 0>), grid, blk, lds, s, a, SR);
+  else if (a.res_mode == 1) hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 1, true, 0>), grid, blk, lds, s, a, SR);
+  else hipLaunchKernelGGL((conv_strip_kernel<T, FC, W, CIN, MPI, 2, true, 0>), grid, blk, lds, s, a, SR);
   return hipGetLastError();
 }
 
 // mpi: pixels per iteration (128 -> 4 waves, 256 -> 8 waves = two per SIMD)
+// the specialised shapes SH = 1 .. kNStripShapes-1 (16-bit storage only) matching the launch
+template <typename T, int SH>
+static bool strip_shape_go(const ConvArgs& a, int nblk, int mpi, int SR, int B, hipStream_t s, hipError_t& e) {
+  if constexpr (SH >= kNStripShapes || sizeof(T) == 4) {
+    return false;
+  } else {
+    constexpr ConvShape c = kStripShapes[SH];
+    if (strip_shape_matches(c, nblk, mpi, SR, a)) {
+      e = strip_go<T, c.cfg / 16, c.Wo, c.CA + c.CB, c.nw, SH>(a, SR, B, s, nullptr);
+      return true;
+    }
+    return strip_shape_go<T, SH + 1>(a, nblk, mpi, SR, B, s, e);
+  }
+}
+
 template <typename T>
 hipError_t strip_dispatch(const ConvArgs& a, int nblk, int mpi, int SR, int B, hipStream_t s, size_t* lo) {
+  static const bool generic = std::getenv("SDDM_NO_STRIP_SHAPES") != nullptr;   // A/B runs
+  hipError_t e;
+  if (!lo && !generic && strip_shape_go<T, 1>(a, nblk, mpi, SR, B, s, e)) return e;
   const int Cin = a.CA + a.CB;
 #define SDDM_STRIP(FCV, WV, CV)                                                                   \
   if (nblk == 16 * FCV && a.Wo == WV && Cin == CV)                                                \

@@ -862,10 +862,11 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       const ConvChoice ch = st.ch;
       const bool s2 = st.s2 != 0;
       const bool temb = st.temb;
-      if (std::getenv("SDDM_PRINT_SHAPES") && !ch.strip)   // rows for kTileShapes / kDeepShapes
-        fprintf(stderr, "SHAPE %s %s%d s2=%d TR=%d TW=%d Ho=%d Wo=%d CA=%d CB=%d Cout=%d RCA=%d RCB=%d res=%d gn=%d up=%d mt=%d nw=%d nb=%d\n",
-                st.w.c_str(), ch.tile >= 0 ? "tile" : "deep", ch.tile >= 0 ? ch.tile : ch.mt, s2 ? 1 : 0, a.TR, a.TW, a.Ho,
-                a.Wo, a.CA, a.CB, a.Cout, a.RCA, a.RCB, a.res_mode, a.gamma ? 1 : 0, a.upsample ? 1 : 0, ch.mt, ch.nw, ch.nb);
+      if (std::getenv("SDDM_PRINT_SHAPES"))   // rows for kTileShapes / kDeepShapes / kStripShapes
+        fprintf(stderr, "SHAPE %s %s%d s2=%d TR=%d TW=%d Ho=%d Wo=%d CA=%d CB=%d Cout=%d RCA=%d RCB=%d res=%d gn=%d up=%d mt=%d nw=%d nb=%d nblk=%d mpi=%d SR=%d ntiles=%d\n",
+                st.w.c_str(), ch.strip ? "strip" : (ch.tile >= 0 ? "tile" : "deep"), ch.tile >= 0 ? ch.tile : ch.mt, s2 ? 1 : 0,
+                a.TR, a.TW, a.Ho, a.Wo, a.CA, a.CB, a.Cout, a.RCA, a.RCB, a.res_mode, a.gamma ? 1 : 0, a.upsample ? 1 : 0,
+                ch.mt, ch.nw, ch.nb, ch.nblk, ch.mpi, ch.SR, a.n_tiles);
       const int toff = temb ? c->temb_off.at(st.rb) : 0;
 #ifdef SDDM_STAMPS
       if (const char* sn = std::getenv("SDDM_STAMPS")) {
