@@ -150,7 +150,8 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;
 
   int tile, b, zb;
-  xcd_block(gNT, gCout / NB, tile, b, zb);
+  if (a.deep_zin) xcd_block<true>(gNT, gCout / NB, tile, b, zb);
+  else xcd_block<false>(gNT, gCout / NB, tile, b, zb);
   const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int n0 = zb * NB;

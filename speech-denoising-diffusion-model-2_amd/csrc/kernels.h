@@ -69,7 +69,7 @@ struct ConvArgs {
   const void* res_wgt;        // packed [Cout_pad][RCA+RCB] (T)
   void* out;                  // [B][Ho][Wo][Cout]
   float* stats;               // [B][n_tiles][Cout][2] (sum, M2 about tile mean) or null
-  int ck_batch;               // (unused: conv_deep stages every input chunk at once)
+  int deep_zin;               // conv_deep: 1 = a tile's channel blocks on one XCD (input halo from L2), 0 = z-major
   int deep_nw;                // conv_deep: waves per block (4: two blocks per CU, 8: one)
   int deep_nb;                // conv_deep: output channels per block (32 or 16; 0 = 32)
   unsigned long long* stamps; // SDDM_STAMPS builds only: per-block phase timestamps [blocks][8]

@@ -384,15 +384,25 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
   constexpr bool CS = SH > 0;
   const int FT = CS ? FS.FT : a.FT, Ns = CS ? FS.N : a.N;
   const int mode = MODE != kFinalModeArg ? MODE : a.mode;
-  const int b = blockIdx.y, f0 = blockIdx.x * FT, tid = threadIdx.x;
   const int C = CS ? FS.C : a.C, W = CS ? FS.W : a.W, S = CS ? FS.S : a.S, F = CS ? FS.F : a.F;
+  // frame tile and image: a 1-D grid is dealt to the XCDs in the order of xcd_block (the frame
+  // tiles of an image on one XCD, so the halo frames a tile shares with its neighbours come from
+  // that XCD's L2); a 2-D grid is (tile, image)
+  int ftile, b;
+  if (gridDim.y == 1) {
+    int zz;
+    xcd_block<true>(F / FT, 1, ftile, b, zz);
+  } else {
+    ftile = blockIdx.x; b = blockIdx.y;
+  }
+  const int f0 = ftile * FT, tid = threadIdx.x;
   const int back = W / S - 1;                 // extra frames before f0 needed by the OLA
   const int YR = FT + back;                   // y rows: frames [f0-back, f0+FT)
   const int PR = YR + 2, PC = W + 2;          // partial-product rows / cols (zero halo cols)
   float* P = (float*)smem;                    // [9][PR][PC]
   float* y = P + 9 * PR * PC;                 // [YR][W]
   float* gs = y + YR * W;                     // [2][C]
-  SDDM_STAMP_AT(a, 0, blockIdx.x + blockIdx.y * (F / FT));
+  SDDM_STAMP_AT(a, 0, ftile + b * (F / FT));
   // every independent load first: the transition's x_t / condition (one 4-sample vector per
   // thread: the block's samples fit one pass, checked by the launcher), the GroupNorm statistics
   // and the first pass of activation fragments; then one wait
@@ -439,7 +449,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
   load_pass(wave);
   gl.finish(gf, b, C, 0, gs, gs + C);
   lds_sync();                                        // scale / shift visible (loads stay in flight)
-  SDDM_STAMP_AT(a, 1, blockIdx.x + blockIdx.y * (F / FT));
+  SDDM_STAMP_AT(a, 1, ftile + b * (F / FT));
   // SiLU through exp2 with the constants folded: t = -(x sc + sh) log2(e) = x sc' + sh', and
   // silu = -ln2 * t / (1 + 2^t); the -ln2 goes into the fp32 weights (one multiply per lane)
   constexpr float kL2E = 1.4426950408889634f, kLN2 = 0.6931471805599453f;
@@ -497,7 +507,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
   }
   }
   lds_sync();
-  SDDM_STAMP_AT(a, 2, blockIdx.x + blockIdx.y * (F / FT));
+  SDDM_STAMP_AT(a, 2, ftile + b * (F / FT));
   for (int p = tid; p < YR * W; p += NT) {
     const int r = p / W, w = p - r * W;        // y row r <-> P rows r .. r+2, cols w .. w+2
     float s = 0.f;
@@ -508,7 +518,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
     y[p] = s + a.bias;
   }
   lds_sync();
-  SDDM_STAMP_AT(a, 3, blockIdx.x + blockIdx.y * (F / FT));
+  SDDM_STAMP_AT(a, 3, ftile + b * (F / FT));
   const int t = a.t_dev ? *a.t_dev : 0;
   const uint64_t seed = a.sp ? a.sp->seed : a.seed;
   const int64_t row_offset = a.sp ? a.sp->row_offset : a.row_offset;
@@ -557,8 +567,8 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
         for (int j = 0; j < 4 && n4 + j < n_end; ++j) xrow[n4 + j] = o[j];
     }
   }
-  SDDM_STAMP_AT(a, 6, blockIdx.x + blockIdx.y * (F / FT));
-  SDDM_STAMP_AT(a, 7, blockIdx.x + blockIdx.y * (F / FT));
+  SDDM_STAMP_AT(a, 6, ftile + b * (F / FT));
+  SDDM_STAMP_AT(a, 7, ftile + b * (F / FT));
 }
 
 hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
@@ -569,7 +579,8 @@ hipError_t launch_final(int dtype, const FinalArgs& a, int B, hipStream_t s) {
   // samples (the last block's tail included)
   const int nt = a.FT >= 16 ? 1024 : 512;
   if (lds > kLdsBytes || a.F % a.FT || a.C != 32 || a.FT * a.S + a.W > 4 * nt || a.N % 4) return hipErrorInvalidValue;
-  dim3 grid(a.F / a.FT, B);
+  static const bool xcd = !std::getenv("SDDM_FINAL_XCD") || std::atoi(std::getenv("SDDM_FINAL_XCD")) != 0;
+  const dim3 grid = xcd ? dim3((a.F / a.FT) * B) : dim3(a.F / a.FT, B);
   static const bool generic = std::getenv("SDDM_NO_FINAL_SHAPES") != nullptr;   // A/B runs
   constexpr FinalShape h = kFinalShapes[1];
   const bool shaped = !generic && dtype != DT_F32 && nt == 512 && a.FT == h.FT && a.W == h.W && a.S == h.S &&

@@ -557,6 +557,19 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
 // element and weight) among those whose grid still fills the chip; when no tile reaches 256
 // blocks, the one with the most blocks.  SDDM_TILE_CFG=<i> forces configuration i wherever it
 // fits; SDDM_NO_TILE=1 keeps every 16-bit layer on conv_deep (experiments).
+// conv_deep block order: a tile's channel blocks on one XCD (the input halo read once per XCD,
+// every XCD reading every weight slice) when the layer's input is at least its weights, else
+// z-major (each XCD its own weight slices; the 8x4 / 16x8 levels, where weights dominate).  PMC:
+// deep-level traffic 200.6 MB (z-major everywhere) -> 138.6 (channel-inner everywhere) -> ~130 MB
+// per step.  SDDM_DEEP_ZIN=0/1 forces one order (A/B runs).
+static int deep_zin(const ConvArgs& a, int B, size_t es) {
+  static const int force = std::getenv("SDDM_DEEP_ZIN") ? std::atoi(std::getenv("SDDM_DEEP_ZIN")) : -1;
+  if (force >= 0) return force;
+  const double in = (double)B * a.Hi * a.Wi * (a.CA + a.CB) * es;
+  const double w = (double)a.Cout * ((a.CA + a.CB) * 9 + (a.res_mode == 2 ? a.RCA + a.RCB : 0)) * es;
+  return in >= w ? 1 : 0;
+}
+
 static bool choose_tile(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int want = -1) {
   if (dt == DT_F32) return false;
   static const int force = std::getenv("SDDM_TILE_CFG") ? std::atoi(std::getenv("SDDM_TILE_CFG")) : -1;
@@ -892,7 +905,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
                           }
                           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
                           if (ch.tile >= 0) return launch_conv_tile(dt, ch.tile, s2, x, B, s);
-                          x.ck_batch = ch.ckb; x.deep_nw = ch.nw; x.deep_nb = ch.nb;
+                          x.deep_zin = deep_zin(x, B, dtype_size(dt)); x.deep_nw = ch.nw; x.deep_nb = ch.nb;
                           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
                         }, st.w + (ch.strip ? "[strip]" : (ch.tile >= 0 ? "[tile" + std::to_string(ch.tile) + "]"
                                                                          : "[deep" + std::to_string(ch.mt) + "_" + std::to_string(ch.nw) + "_" + std::to_string(ch.nb) + "]"))});
@@ -933,7 +946,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           x.dbg = fl;
           if (ch.strip) return launch_conv_strip(dt, ch.nblk, ch.mpi, ch.SR, x, B, s);
           if (ch.tile >= 0) return launch_conv_tile(dt, ch.tile, s2, x, B, s);
-          x.ck_batch = ch.ckb; x.deep_nw = ch.nw; x.deep_nb = ch.nb;
+          x.deep_zin = deep_zin(x, B, dtype_size(dt)); x.deep_nw = ch.nw; x.deep_nb = ch.nb;
           return launch_conv_deep(dt, ch.mt, s2, x, B, s);
         };
         (void)base;

@@ -1,6 +1,7 @@
 # round evidence: PMC traffic, headline bench (T=1000, CPU baseline), rocprofv3 kernel stats of the
 # same workload (T=100), fp32 config #2 throughput, DiffWave and WaveGrad benches + kernel stats.
-# Usage: ROUND=r02 bash tools/gpu_round_profiles.sh ; results land in gpurun_out/profiles/
+# fp16 twin of the headline; with CONFIG5=1 also config #5's PMC traffic and per-GPU bench.
+# Usage: ROUND=r05 CONFIG5=1 bash tools/gpu_round_profiles.sh ; results land in gpurun_out/profiles/
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -14,8 +15,17 @@ timeout -k 10 900 python3 bench.py > $O/${R}_bench.json.log 2>&1 || { echo BENCH
 tail -1 $O/${R}_bench.json.log | cut -c1-200
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_bench -o run -- python3 bench.py --timesteps 100 --steps 1 --warmup 1 --no-cpu-baseline > $O/${R}_bench_T100_rocprof.json.log 2>&1 || { echo PROF_FAIL; exit 1; }
 cp gpurun_out/prof_bench/run_kernel_stats.csv $O/${R}_kernel_stats_T100_B16_bf16.csv
+timeout -k 10 900 python3 bench.py --dtype f16 --no-cpu-baseline > $O/${R}_bench_f16.json.log 2>&1 || { echo F16_FAIL; exit 1; }
+tail -1 $O/${R}_bench_f16.json.log | cut -c1-200
 timeout -k 10 900 python3 bench.py --dtype f32 --no-cpu-baseline > $O/${R}_unet_fp32_bench.json.log 2>&1 || { echo FP32_FAIL; exit 1; }
 tail -1 $O/${R}_unet_fp32_bench.json.log | cut -c1-200
+if [ -n "$CONFIG5" ]; then   # config #5 per GPU: PMC traffic, then the bench line that reads it
+  OPS_ARGS="--batch 128 --num-samples 32832 --dtype f16 --lane-rows 64" TRAFFIC_KEY="32832 128 f16" \
+    TRAFFIC_OUT=profiles/${R}_config5_hbm_traffic.json bash tools/gpu_traffic.sh || { echo C5_TRAFFIC_FAIL; exit 1; }
+  cp profiles/${R}_config5_hbm_traffic.json $O/
+  timeout -k 10 900 python3 bench.py --batch 128 --num-samples 32832 --dtype f16 --no-cpu-baseline > $O/${R}_unet_config5_per_gpu_bench.json.log 2>&1 || { echo C5_FAIL; exit 1; }
+  tail -1 $O/${R}_unet_config5_per_gpu_bench.json.log | cut -c1-200
+fi
 timeout -k 10 900 python3 bench.py --workload diffwave > $O/${R}_diffwave_bench.json.log 2>&1 || { echo DW_FAIL; tail -5 $O/${R}_diffwave_bench.json.log; exit 1; }
 tail -1 $O/${R}_diffwave_bench.json.log | cut -c1-200
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_dw -o run -- python3 bench.py --workload diffwave --timesteps 10 --steps 1 --warmup 1 --no-cpu-baseline > $O/${R}_diffwave_T10_rocprof.json.log 2>&1 || { echo PROF_DW_FAIL; exit 1; }
