@@ -63,8 +63,10 @@ template <typename T> __device__ __forceinline__ Frag<T> zero_frag() {
   return pack8<T>(z);
 }
 
+// (0 <= t < 2^21: t / f through the float reciprocal, exact by fdivi's margin, instead of an
+// integer division sequence per staged element; the reciprocal of the uniform f is hoisted)
 __device__ __forceinline__ int wg_map(int t, int map, int f) {
-  return map == WG_MAP_UP ? t / f : (map == WG_MAP_DOWN ? t * f : t);
+  return map == WG_MAP_UP ? fdivi(t, 1.0f / (float)f) : (map == WG_MAP_DOWN ? t * f : t);
 }
 
 // epilogue FiLM of the next conv's input (wavegrad.py:98-99, 104-105, 107-108): m = leaky(shift +
