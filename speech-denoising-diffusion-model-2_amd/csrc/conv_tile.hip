@@ -12,10 +12,11 @@
 //     channel block (once per pixel for most layers), and up to 256 output pixels, so the weights
 //     a block streams are reused by that many pixels;
 //   * K runs in 32-channel chunks through a two-deep pipeline with one barrier per chunk: while
-//     the MFMAs of chunk k run, the raw input halo of chunk k+1 streams into registers and its
-//     weights into LDS by LDS-DMA (global_load_lds: no VGPRs, pre-packed chunk-major in
-//     ConvArgs::wgt_t so every DMA wave-instruction moves one contiguous 1 KiB run); after the
-//     MFMAs the same waves apply GroupNorm + SiLU to chunk k+1 and write its operand image;
+//     the MFMAs of chunk k run, the raw input halo of chunk k+1 and its weights (pre-packed
+//     chunk-major in ConvArgs::wgt_t: every wave-instruction reads one contiguous 1 KiB run)
+//     stream into registers; after the MFMAs the same waves apply GroupNorm + SiLU to chunk k+1
+//     and write its operand image and weight chunk to LDS (round 5: the weights had gone by
+//     LDS-DMA, whose per-unit issue cost made the chunk loop slower, SDDM_TILE_WREG);
 //   * 8-wave blocks keep two waves per SIMD, so one wave's VALU transform overlaps the other's
 //     MFMAs.
 // LDS operand images are plane-major (a plane = 8 channels, 16 B per pixel or output channel);
@@ -29,6 +30,13 @@
 #include "conv_common.h"
 #include "conv_tile_cfg.h"
 #include "kernels.h"
+
+#ifndef SDDM_TILE_WREG
+// 1: weight chunks through registers + ds_write_b128 (default; one global load and one LDS store
+// per 16-byte unit issue cheaper than one LDS-DMA per unit: tile launches -3..-8 us per step,
+// bench +1 %); 0: by LDS-DMA (A/B builds)
+#define SDDM_TILE_WREG 1
+#endif
 
 namespace sddm {
 
@@ -173,6 +181,32 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
       glds16(ws + ((size_t)r * gCout + n0 + co) * 16, dst + u0 * 16);
     }
   };
+#if SDDM_TILE_WREG
+  // weight chunk k through registers: WU 16-byte units per thread, loaded with the raw halo at the
+  // top of an iteration and written to WB[buf] after the MFMAs, beside the transform
+  constexpr int WU = (36 * NB + NT - 1) / NT;
+  f32x4 wr[WU];
+  auto load_w = [&](int k) {
+    const bool res = k >= nck;
+    const int nw = (res ? 4 : 36) * NB;
+    const char* ws = res ? (const char*)a.res_wgt_t + (size_t)(k - nck) * 4 * gCout * 16
+                         : (const char*)a.wgt_t + (size_t)k * 36 * gCout * 16;
+#pragma unroll
+    for (int i = 0; i < WU; ++i) {
+      const int u = tid + i * NT, uu = u < nw ? u : 0, r = uu / NB, co = uu - r * NB;
+      wr[i] = *(const f32x4*)(ws + ((size_t)r * gCout + n0 + co) * 16);
+    }
+  };
+  auto store_w = [&](int k, int buf) {
+    const int nw = (k >= nck ? 4 : 36) * NB;
+    char* dst = WB + buf * WCH;
+#pragma unroll
+    for (int i = 0; i < WU; ++i) {
+      const int u = tid + i * NT;
+      if (u < nw) *(f32x4*)(dst + u * 16) = wr[i];
+    }
+  };
+#endif
   // chunk k: registers -> IB[buf] with zero padding and GroupNorm + SiLU (3x3 chunks of a Block)
   auto transform = [&](int k, int buf) {
     char* ib = IB + buf * geo.ibb;
@@ -252,12 +286,21 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   };
 
   load_raw(0);
+#if SDDM_TILE_WREG
+  load_w(0);
+#else
   issue_w(0, 0);
+#endif
   if (gn) gl.finish(gf, b, gCA, gCB, gsc, gsc + Cin);
   SDDM_STAMP(a, 1);
   __syncthreads();                                         // gsc visible
   transform(0, 0);
+#if SDDM_TILE_WREG
+  store_w(0, 0);
+  lds_sync();
+#else
   dma_sync();                                              // operand image 0, weights 0 (LDS-DMA)
+#endif
   SDDM_STAMP(a, 2);
 #ifdef SDDM_STAMPS
   // timing ablations of the profiling build (SDDM_STAMPS_DBG): 4 no raw loads, 32 no weight DMA,
@@ -268,6 +311,18 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
 #endif
   for (int k = 0; k < nk; ++k) {
     const int cur = k & 1, nxt = cur ^ 1;
+#if SDDM_TILE_WREG
+    if (k + 1 < nk) {
+      if (!(dbg & 4)) load_raw(k + 1);                     // in flight during the MFMAs
+      if (!(dbg & 32)) load_w(k + 1);
+    }
+    if (!(dbg & 8)) mma(k, cur);
+    if (k + 1 < nk) {
+      if (!(dbg & 2)) transform(k + 1, nxt);               // IB[nxt] / WB[nxt] were read by chunk k - 1
+      if (!(dbg & 32)) store_w(k + 1, nxt);
+    }
+    lds_sync();
+#else
     if (k + 1 < nk) {
       if (!(dbg & 4)) load_raw(k + 1);                     // in flight during the MFMAs
       if (!(dbg & 32)) issue_w(k + 1, nxt);                // WB[nxt] was read by chunk k - 1
@@ -275,6 +330,7 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     if (!(dbg & 8)) mma(k, cur);
     if (k + 1 < nk && !(dbg & 2)) transform(k + 1, nxt);   // IB[nxt] was read by chunk k - 1
     dma_sync();                                            // WB[nxt] landed by LDS-DMA from every wave
+#endif
   }
   SDDM_STAMP(a, 4);
 

@@ -71,3 +71,41 @@ def test_two_ranks_on_the_library_equal_single_run(tmp_path):
     a, b = np.load(sharded), np.load(single)
     assert a.shape == (B, 1, N) and np.isfinite(a).all()
     assert np.array_equal(a, b)
+
+
+def _rccl_rank(rank, port, out_path):
+    _paths()
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)   # RCCL on ROCm
+    assert dist.get_backend() == "nccl"
+    from model.model import _all_gather_rows
+    from sddm_hip.synth import noisy_speech
+    seed = torch.tensor([13], dtype=torch.int64, device=dev)
+    dist.broadcast(seed, src=0)                       # the seed hand-out of sharded_infer
+    out = _model().infer(torch.from_numpy(noisy_speech(B, N, seed=4321)).cuda(), seed=int(seed.item()), row_offset=0)
+    gathered = _all_gather_rows(out, None)            # all_gather_into_tensor on device buffers
+    torch.cuda.synchronize()
+    np.save(out_path, gathered.cpu().numpy())
+    dist.destroy_process_group()
+
+
+def test_rccl_collectives_of_the_sharded_path(tmp_path):
+    """The RCCL (torch 'nccl' backend) calls of the multi-GPU path on the MI355X itself: a world-1
+    group, sharded_infer's seed broadcast of a device tensor and _all_gather_rows'
+    all_gather_into_tensor of the sampled rows; the gathered rows equal a single-process run bit
+    for bit.  (RCCL refuses two ranks on one device; the 1/2/4/8-GPU curve is the driver's run.)"""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    rccl, single = str(tmp_path / "rccl.npy"), str(tmp_path / "single.npy")
+    mp.spawn(_rccl_rank, args=(port, rccl), nprocs=1, join=True)
+    mp.spawn(_single, args=(single,), nprocs=1, join=True)
+    a, b = np.load(rccl), np.load(single)
+    assert a.shape == (B, 1, N) and np.isfinite(a).all()
+    assert np.array_equal(a, b)
