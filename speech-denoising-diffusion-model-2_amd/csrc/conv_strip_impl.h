@@ -37,6 +37,9 @@
 #ifndef SDDM_ABL_STRIP
 #define SDDM_ABL_STRIP 0
 #endif
+#ifndef SDDM_STRIP_WLD
+#define SDDM_STRIP_WLD 1   // 0: weight slabs by LDS-DMA only (A/B builds)
+#endif
 #ifndef SDDM_STRIP_WREG
 #define SDDM_STRIP_WREG 1   // 0: weight fragments re-read from LDS every iteration (A/B builds)
 #endif
@@ -142,34 +145,68 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR_
     const bool fa = c0 < gCA;
     ini[k] = *(const f32x4*)((fa ? srcAb : srcBb) + ((size_t)sy * gWi + sx) * (fa ? gCA : gCB) + (fa ? c0 : c0 - gCA));
   }
-  // weight slabs straight into LDS (LDS-DMA: unit u lands at byte 16 u, co fastest, so every
-  // wave-instruction fills 1 KiB of consecutive LDS; no VGPRs, no wait until the first barrier)
-  // NBLK * WPLANES and NBLK * RPLANES are multiples of 64: whole waves, no tail.  16-bit weights
-  // come from the chunk-major image ConvArgs::wgt_t ([Cin/32][9][4][Cout][8]), where the NBLK
-  // channels of one plane are one contiguous run: a wave-instruction reads 1 KiB of consecutive
-  // bytes (8 cache lines).  From the per-channel image (fp32) each lane reads another channel's
-  // row, 32-64 lines per instruction, and the LDS-DMA path takes ~3.5x as long (tools/mb_dma.hip).
-  for (int u0 = wave * 64; u0 < NBLK * WPLANES; u0 += NT) {
-    const int u = u0 + lane;
-    const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
-    const char* src;
-    if constexpr (ES == 2) {
-      src = (const char*)a.wgt_t + ((size_t)pl * gCout + n0 + co) * 16;
-    } else {
-      const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
-      src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
+  // weight slabs: through registers (WLD: WU / RU fixed 16-byte units per thread, clamped loads,
+  // written to LDS after the initial ring rows; a global load + ds_write per unit issues cheaper
+  // than an LDS-DMA, strips -4..-6 us per step, bench +1 %), or, for slabs of more
+  // than 12 units per thread (Cin = 128: too many VGPRs), by LDS-DMA.  Unit u lands at byte 16 u,
+  // co fastest.  16-bit weights come from the chunk-major image ConvArgs::wgt_t
+  // ([Cin/32][9][4][Cout][8]): the NBLK channels of one plane are one contiguous run, so a
+  // wave-instruction reads 1 KiB of consecutive bytes.  From the per-channel image (fp32) each
+  // lane reads another channel's row.
+  constexpr int WUN = NBLK * WPLANES, WU = (WUN + NT - 1) / NT;
+  constexpr bool WLD = SDDM_STRIP_WLD && WU <= 12;
+  constexpr int RUN_MAX = RES == 2 ? NBLK * RCKM * 4 * UPL : 0, RU = (RUN_MAX + NT - 1) / NT;
+  const int RUN = NBLK * RPLANES;
+  f32x4 wst[WLD ? WU : 1], rst[WLD && RU > 0 ? RU : 1];
+  if constexpr (WLD) {
+#pragma unroll
+    for (int i = 0; i < WU; ++i) {
+      const int u0 = tid + i * NT, u = u0 < WUN ? u0 : 0;
+      const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
+      const char* src;
+      if constexpr (ES == 2) {
+        src = (const char*)a.wgt_t + ((size_t)pl * gCout + n0 + co) * 16;
+      } else {
+        const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
+        src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
+      }
+      wst[i] = *(const f32x4*)src;
     }
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                     (__attribute__((address_space(3))) void*)(wl + u0 * 16), 16, 0, 0);
-  }
-  if constexpr (RES == 2) {
-    for (int u0 = wave * 64; u0 < NBLK * RPLANES; u0 += NT) {
+    if constexpr (RES == 2) {
+#pragma unroll
+      for (int i = 0; i < RU; ++i) {
+        const int u0 = tid + i * NT, u = u0 < RUN ? u0 : 0;
+        const int co = u % NBLK, pl = u / NBLK;
+        const char* src = ES == 2 ? (const char*)a.res_wgt_t + ((size_t)pl * gCout + n0 + co) * 16
+                                  : (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
+        rst[i] = *(const f32x4*)src;
+      }
+    }
+  } else {
+    // LDS-DMA: every wave-instruction fills 1 KiB of consecutive LDS, no VGPRs, no wait until the
+    // first barrier; NBLK * WPLANES and NBLK * RPLANES are multiples of 64: whole waves, no tail
+    for (int u0 = wave * 64; u0 < NBLK * WPLANES; u0 += NT) {
       const int u = u0 + lane;
-      const int co = u % NBLK, pl = u / NBLK;
-      const char* src = ES == 2 ? (const char*)a.res_wgt_t + ((size_t)pl * gCout + n0 + co) * 16
-                                : (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
+      const int co = u % NBLK, pl = u / NBLK;                 // pl = (ck*9 + tap)*4*UPL + unit
+      const char* src;
+      if constexpr (ES == 2) {
+        src = (const char*)a.wgt_t + ((size_t)pl * gCout + n0 + co) * 16;
+      } else {
+        const int ck = pl / (9 * 4 * UPL), rem = pl - ck * 9 * 4 * UPL, tap = rem / (4 * UPL), un = rem - tap * 4 * UPL;
+        src = (const char*)a.wgt + ((((size_t)(n0 + co) * NCK + ck) * 9 + tap) * 32) * ES + un * 16;
+      }
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                       (__attribute__((address_space(3))) void*)(rw + u0 * 16), 16, 0, 0);
+                                       (__attribute__((address_space(3))) void*)(wl + u0 * 16), 16, 0, 0);
+    }
+    if constexpr (RES == 2) {
+      for (int u0 = wave * 64; u0 < NBLK * RPLANES; u0 += NT) {
+        const int u = u0 + lane;
+        const int co = u % NBLK, pl = u / NBLK;
+        const char* src = ES == 2 ? (const char*)a.res_wgt_t + ((size_t)pl * gCout + n0 + co) * 16
+                                  : (const char*)a.res_wgt + ((size_t)(n0 + co) * RC) * ES + pl * 16;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                         (__attribute__((address_space(3))) void*)(rw + u0 * 16), 16, 0, 0);
+      }
     }
   }
   for (int u = tid; u < R * UPP * 2; u += NT) {           // zero halo columns
@@ -210,6 +247,17 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR_
     if (ry < 0 || ry >= H) v = f32x4{0.f, 0.f, 0.f, 0.f};
     else if (gn) v = transform_fast<T>(v, gsc + q * VE, gsc + CIN + q * VE);
     *(f32x4*)(ring + ((base + r) % R) * SLOT + q * PL + (x + 1) * 16) = v;
+  }
+
+  if constexpr (WLD) {
+#pragma unroll
+    for (int i = 0; i < WU; ++i)
+      if (tid + i * NT < WUN) *(f32x4*)(wl + (tid + i * NT) * 16) = wst[i];
+    if constexpr (RES == 2) {
+#pragma unroll
+      for (int i = 0; i < RU; ++i)
+        if (tid + i * NT < RUN) *(f32x4*)(rw + (tid + i * NT) * 16) = rst[i];
+    }
   }
 
   // a 16-pixel column fragment never crosses a row (W % 16 == 0), so its row is wave-uniform: the
