@@ -181,11 +181,13 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
       glds16(ws + ((size_t)r * gCout + n0 + co) * 16, dst + u0 * 16);
     }
   };
-#if SDDM_TILE_WREG
-  // weight chunk k through registers: WU 16-byte units per thread, loaded with the raw halo at the
-  // top of an iteration and written to WB[buf] after the MFMAs, beside the transform
+  // weight chunk k through registers (WR): WU 16-byte units per thread, loaded with the raw halo
+  // at the top of an iteration and written to WB[buf] after the MFMAs, beside the transform.  The
+  // generic (runtime-geometry) instantiations with more than 6 accumulator fragments per wave keep
+  // LDS-DMA: the extra registers made them spill (config #5's 256-pixel x 96-channel tiles)
+  constexpr bool WR = SDDM_TILE_WREG && (SH > 0 || FP * FC <= 6);
   constexpr int WU = (36 * NB + NT - 1) / NT;
-  f32x4 wr[WU];
+  f32x4 wr[WR ? WU : 1];
   auto load_w = [&](int k) {
     const bool res = k >= nck;
     const int nw = (res ? 4 : 36) * NB;
@@ -206,7 +208,6 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
       if (u < nw) *(f32x4*)(dst + u * 16) = wr[i];
     }
   };
-#endif
   // chunk k: registers -> IB[buf] with zero padding and GroupNorm + SiLU (3x3 chunks of a Block)
   auto transform = [&](int k, int buf) {
     char* ib = IB + buf * geo.ibb;
@@ -286,21 +287,18 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
   };
 
   load_raw(0);
-#if SDDM_TILE_WREG
-  load_w(0);
-#else
-  issue_w(0, 0);
-#endif
+  if constexpr (WR) load_w(0);
+  else issue_w(0, 0);
   if (gn) gl.finish(gf, b, gCA, gCB, gsc, gsc + Cin);
   SDDM_STAMP(a, 1);
   __syncthreads();                                         // gsc visible
   transform(0, 0);
-#if SDDM_TILE_WREG
-  store_w(0, 0);
-  lds_sync();
-#else
-  dma_sync();                                              // operand image 0, weights 0 (LDS-DMA)
-#endif
+  if constexpr (WR) {
+    store_w(0, 0);
+    lds_sync();
+  } else {
+    dma_sync();                                            // operand image 0, weights 0 (LDS-DMA)
+  }
   SDDM_STAMP(a, 2);
 #ifdef SDDM_STAMPS
   // timing ablations of the profiling build (SDDM_STAMPS_DBG): 4 no raw loads, 32 no weight DMA,
@@ -311,26 +309,26 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
 #endif
   for (int k = 0; k < nk; ++k) {
     const int cur = k & 1, nxt = cur ^ 1;
-#if SDDM_TILE_WREG
-    if (k + 1 < nk) {
-      if (!(dbg & 4)) load_raw(k + 1);                     // in flight during the MFMAs
-      if (!(dbg & 32)) load_w(k + 1);
+    if constexpr (WR) {
+      if (k + 1 < nk) {
+        if (!(dbg & 4)) load_raw(k + 1);                   // in flight during the MFMAs
+        if (!(dbg & 32)) load_w(k + 1);
+      }
+      if (!(dbg & 8)) mma(k, cur);
+      if (k + 1 < nk) {
+        if (!(dbg & 2)) transform(k + 1, nxt);             // IB[nxt] / WB[nxt] were read by chunk k - 1
+        if (!(dbg & 32)) store_w(k + 1, nxt);
+      }
+      lds_sync();
+    } else {
+      if (k + 1 < nk) {
+        if (!(dbg & 4)) load_raw(k + 1);                   // in flight during the MFMAs
+        if (!(dbg & 32)) issue_w(k + 1, nxt);              // WB[nxt] was read by chunk k - 1
+      }
+      if (!(dbg & 8)) mma(k, cur);
+      if (k + 1 < nk && !(dbg & 2)) transform(k + 1, nxt); // IB[nxt] was read by chunk k - 1
+      dma_sync();                                          // WB[nxt] landed by LDS-DMA from every wave
     }
-    if (!(dbg & 8)) mma(k, cur);
-    if (k + 1 < nk) {
-      if (!(dbg & 2)) transform(k + 1, nxt);               // IB[nxt] / WB[nxt] were read by chunk k - 1
-      if (!(dbg & 32)) store_w(k + 1, nxt);
-    }
-    lds_sync();
-#else
-    if (k + 1 < nk) {
-      if (!(dbg & 4)) load_raw(k + 1);                     // in flight during the MFMAs
-      if (!(dbg & 32)) issue_w(k + 1, nxt);                // WB[nxt] was read by chunk k - 1
-    }
-    if (!(dbg & 8)) mma(k, cur);
-    if (k + 1 < nk && !(dbg & 2)) transform(k + 1, nxt);   // IB[nxt] was read by chunk k - 1
-    dma_sync();                                            // WB[nxt] landed by LDS-DMA from every wave
-#endif
   }
   SDDM_STAMP(a, 4);
 
