@@ -1,0 +1,72 @@
+"""CPU: the compile-time layer-shape tables (conv_tile_cfg.h kTileShapes, conv_deep.hip kDeepShapes,
+conv_strip_impl.h kStripShapes; DESIGN.md §3 "Compile-time layer shapes") agree with the measured
+per-layer kernel table (configs/conv_tuning.json) and cover every conv of the headline plan.  A
+row that drifts from the table is never wrong (the launch falls back to the generic kernel when a
+field differs) but silently loses the specialisation, so the drift is caught here."""
+import json
+import os
+import re
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CSRC = os.path.join(REPO, "speech-denoising-diffusion-model-2_amd", "csrc")
+TUNING = os.path.join(REPO, "speech-denoising-diffusion-model-2_amd", "configs", "conv_tuning.json")
+FIELDS = ("cfg", "s2", "TR", "TW", "Ho", "Wo", "CA", "CB", "Cout", "RCA", "RCB", "res", "gn", "up", "nw", "nb")
+
+
+def _rows(path, table):
+    src = open(os.path.join(CSRC, path)).read()
+    body = src[src.index(f"static constexpr ConvShape {table}[] = {{"):]
+    body = body[:body.index("\n};")]
+    rows = []
+    for m in re.finditer(r"\{([-\d,\s]+)\},\s*//\s*(\S+)", body):
+        vals = [int(v) for v in m.group(1).split(",")]
+        row = dict(zip(FIELDS, vals + [0] * (len(FIELDS) - len(vals))))
+        rows.append((m.group(2), row))
+    return rows
+
+
+def _tables():
+    return {"tile": _rows("conv_tile_cfg.h", "kTileShapes"), "deep": _rows("conv_deep.hip", "kDeepShapes"),
+            "strip": _rows("conv_strip_impl.h", "kStripShapes")}
+
+
+def test_generic_entry_first():
+    for kind, rows in _tables().items():
+        assert rows[0][0] == "generic" and rows[0][1]["cfg"] == -1, kind
+
+
+def test_rows_match_the_measured_kernel_table():
+    tuning = json.load(open(TUNING))
+    assert tuning["num_samples"] == 16448 and tuning["lane_batch"] == 16   # the geometry the rows encode
+    kern = tuning["kernel"]
+    for kind, rows in _tables().items():
+        for name, r in rows[1:]:
+            assert name in kern, f"{kind} shape row {name} names no layer of the tuning table"
+            if kind == "tile":
+                want = f"tile:{r['cfg']}"
+            elif kind == "deep":
+                want = f"deep:{r['cfg']}:{r['nw']}:{r['nb']}"
+            else:
+                want = "strip"
+            assert kern[name] == want, f"{name}: shape row is {want}, tuning table says {kern[name]}"
+
+
+def test_every_tuned_layer_has_exactly_one_shape():
+    kern = json.load(open(TUNING))["kernel"]
+    names = [n for rows in _tables().values() for n, _ in rows[1:]]
+    assert sorted(names) == sorted(kern), set(names) ^ set(kern)
+
+
+def test_row_invariants():
+    for kind, rows in _tables().items():
+        for name, r in rows[1:]:
+            assert r["Ho"] % r["TR"] == 0 and r["Wo"] % r["TW"] == 0, name
+            assert (r["CA"] + r["CB"]) % 32 == 0 and r["Cout"] % 32 == 0, name
+            assert r["res"] in (0, 1, 2) and (r["res"] == 2) == (r["RCA"] + r["RCB"] > 0), name
+            assert not (r["s2"] and r["up"]), name
+            if r["res"]:
+                assert r["gn"] == 1, f"{name}: residual modes are ResnetBlock block2 convs (GroupNorm input)"
+            if kind == "strip":
+                assert r["TR"] == r["nb"] and r["TW"] == r["Wo"], f"{name}: strip rows encode TR = strip rows, TW = W"
+            if kind == "deep":
+                assert r["TR"] * r["TW"] <= r["cfg"] and r["nw"] in (4, 8) and r["nb"] in (16, 32), name
