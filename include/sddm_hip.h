@@ -117,11 +117,12 @@ int sddm_q_sample(sddm_ctx* ctx, int mode, const float* x0, const float* y, cons
                   const int64_t* t, const float* r, int64_t B, int64_t N, float* x_t,
                   float* combined, float* s_out, float* level_out, void* stream);
 
-/* Measured per-layer tiles for the narrow-level conv kernel (no reference counterpart: a tuning
- * table).  json = {"lane_batch": B, "dtype": "bfloat16", "num_samples": N,
- * "deep": {"<layer name>": [pixels_per_block, waves], ...}}; applied at the next plan build when
- * the plan's lane batch / dtype / num_samples match, ignored otherwise (and per layer whenever the
- * requested tile does not fit that layer). */
+/* Measured per-layer conv kernels (no reference counterpart: a tuning table).  json = one table
+ * {"lane_batch": B, "dtype": "bfloat16", "num_samples": N, "kernel": {"<layer name>": "strip" |
+ * "tile:<cfg>" | "deep:<pixels>:<waves>:<channels>", ...}} or {"tables": [table, ...]}; at the next
+ * plan build the first table whose lane batch / dtype / num_samples match the plan applies (a
+ * bfloat16 table also serves float16), none otherwise (and per layer whenever the requested
+ * kernel does not fit that layer). */
 int sddm_set_conv_tuning(sddm_ctx* ctx, const char* json);
 
 /* Replaces the torchaudio featurizer of prepare_spectrogram.py:20-55 (context-free):

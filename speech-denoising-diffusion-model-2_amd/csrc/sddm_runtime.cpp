@@ -292,13 +292,16 @@ struct sddm_ctx {
   // SDDM_spectrogram + DiffWave
   std::shared_ptr<DWState> dws;
   std::shared_ptr<WGState> wgs;
-  // measured conv_deep tiles per layer name: (pixels per block, waves); valid for one lane batch /
-  // dtype / num_samples (sddm_set_conv_tuning)
-  std::map<std::string, std::pair<int, int>> deep_tune;
-  // per-layer kernel choice: 1 strip, 2 tile (a = configuration), 3 deep (a = pixels, b = waves)
+  // measured per-layer kernel tables (sddm_set_conv_tuning), each valid for one lane batch /
+  // dtype / num_samples: conv_deep tiles per layer name (pixels per block, waves) and the kernel
+  // choice (1 strip, 2 tile (a = configuration), 3 deep (a = pixels, b = waves, c = channels))
   struct KernTune { int kind, a, b, c; };
-  std::map<std::string, KernTune> kern_tune;
-  int tune_B = -1, tune_dtype = -1, tune_N = -1;
+  struct TuneTable {
+    std::map<std::string, std::pair<int, int>> deep_tune;
+    std::map<std::string, KernTune> kern_tune;
+    int B = -1, dtype = -1, N = -1;
+  };
+  std::vector<TuneTable> tunes;
   int hop_samples = 256;
 
   const float* dtab(int k) const { return warena.at<float>(off_tables) + (size_t)k * (T + 1); }
@@ -702,16 +705,19 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   // and GroupNorm tilings, hence bit-identical rows
   const int PB = std::max(1, c->lane_rows);
   // (a table measured in bf16 also serves f16: the same kernels at the same bytes and MFMA rate)
-  const bool same_dt = c->tune_dtype == dt || (c->tune_dtype >= 0 && c->tune_dtype != DT_F32 && dt != DT_F32);
-  const bool tuned = c->tune_B == PB && same_dt && c->tune_N == N;
+  const sddm_ctx::TuneTable* tuned = nullptr;
+  for (const auto& tt : c->tunes) {
+    const bool same_dt = tt.dtype == dt || (tt.dtype >= 0 && tt.dtype != DT_F32 && dt != DT_F32);
+    if (tt.B == PB && same_dt && tt.N == N) { tuned = &tt; break; }
+  }
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
     int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;
     if (tuned) {
-      auto it = c->deep_tune.find(name);
-      if (it != c->deep_tune.end()) { wm = it->second.first; wn = it->second.second; kind = 3; }
-      auto kt = c->kern_tune.find(name);
-      if (kt != c->kern_tune.end()) {
+      auto it = tuned->deep_tune.find(name);
+      if (it != tuned->deep_tune.end()) { wm = it->second.first; wn = it->second.second; kind = 3; }
+      auto kt = tuned->kern_tune.find(name);
+      if (kt != tuned->kern_tune.end()) {
         kind = kt->second.kind; ka = kt->second.a;
         if (kind == 3) { wm = kt->second.a; wn = kt->second.b; wb = kt->second.c; }
       }
@@ -1583,32 +1589,47 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
   } catch (const std::exception& e) {
     FAIL(SDDM_ERR_INVALID_ARG, "tuning JSON: %s", e.what());
   }
-  const std::string dts = j.string("dtype", "");
-  const int dt = dts == "float32" ? DT_F32 : dts == "bfloat16" ? DT_BF16 : dts == "float16" ? DT_F16 : -1;
-  c->deep_tune.clear();
-  c->kern_tune.clear();
-  if (j.has("deep"))
-    for (const auto& kv : j.at("deep").obj) {
-      if (kv.second.kind != Json::ARR || kv.second.arr.size() != 2) FAIL(SDDM_ERR_INVALID_ARG, "deep.%s: [mt, nw]", kv.first.c_str());
-      c->deep_tune[kv.first] = {(int)kv.second.arr[0].num, (int)kv.second.arr[1].num};
-    }
-  // "kernel": {"<layer>": "strip" | "tile:<cfg>" | "deep" | "deep:<mt>:<nw>[:<nb>]"}
-  if (j.has("kernel"))
-    for (const auto& kv : j.at("kernel").obj) {
-      if (kv.second.kind != Json::STR) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: a string", kv.first.c_str());
-      const std::string& v = kv.second.str;
-      sddm_ctx::KernTune t{0, 0, 0, 0};
-      if (v == "strip") t.kind = 1;
-      else if (v.rfind("tile:", 0) == 0) { t.kind = 2; t.a = std::atoi(v.c_str() + 5); }
-      else if (v == "deep") t.kind = 3;
-      else if (v.rfind("deep:", 0) == 0) { t.kind = 3; std::sscanf(v.c_str() + 5, "%d:%d:%d", &t.a, &t.b, &t.c); }
-      else FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: unknown choice '%s'", kv.first.c_str(), v.c_str());
-      if (t.kind == 2 && (t.a < 0 || t.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), t.a);
-      c->kern_tune[kv.first] = t;
-    }
-  c->tune_B = (int)j.number("lane_batch", -1);
-  c->tune_dtype = dt;
-  c->tune_N = (int)j.number("num_samples", -1);
+  // one table, or {"tables": [table, ...]}: the plan takes the first whose lane batch, dtype and
+  // length match it (a bf16 table also serves f16 plans)
+  std::vector<const Json*> tabs;
+  if (j.has("tables")) {
+    const Json& arr = j.at("tables");
+    if (arr.kind != Json::ARR) FAIL(SDDM_ERR_INVALID_ARG, "tables: a list");
+    for (const auto& t : arr.arr) tabs.push_back(&t);
+  } else {
+    tabs.push_back(&j);
+  }
+  std::vector<sddm_ctx::TuneTable> out;
+  for (const Json* tp : tabs) {
+    const Json& t = *tp;
+    if (t.kind != Json::OBJ) FAIL(SDDM_ERR_INVALID_ARG, "tuning table: an object");
+    sddm_ctx::TuneTable tt;
+    const std::string dts = t.string("dtype", "");
+    tt.dtype = dts == "float32" ? DT_F32 : dts == "bfloat16" ? DT_BF16 : dts == "float16" ? DT_F16 : -1;
+    if (t.has("deep"))
+      for (const auto& kv : t.at("deep").obj) {
+        if (kv.second.kind != Json::ARR || kv.second.arr.size() != 2) FAIL(SDDM_ERR_INVALID_ARG, "deep.%s: [mt, nw]", kv.first.c_str());
+        tt.deep_tune[kv.first] = {(int)kv.second.arr[0].num, (int)kv.second.arr[1].num};
+      }
+    // "kernel": {"<layer>": "strip" | "tile:<cfg>" | "deep" | "deep:<mt>:<nw>[:<nb>]"}
+    if (t.has("kernel"))
+      for (const auto& kv : t.at("kernel").obj) {
+        if (kv.second.kind != Json::STR) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: a string", kv.first.c_str());
+        const std::string& v = kv.second.str;
+        sddm_ctx::KernTune k{0, 0, 0, 0};
+        if (v == "strip") k.kind = 1;
+        else if (v.rfind("tile:", 0) == 0) { k.kind = 2; k.a = std::atoi(v.c_str() + 5); }
+        else if (v == "deep") k.kind = 3;
+        else if (v.rfind("deep:", 0) == 0) { k.kind = 3; std::sscanf(v.c_str() + 5, "%d:%d:%d", &k.a, &k.b, &k.c); }
+        else FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: unknown choice '%s'", kv.first.c_str(), v.c_str());
+        if (k.kind == 2 && (k.a < 0 || k.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), k.a);
+        tt.kern_tune[kv.first] = k;
+      }
+    tt.B = (int)t.number("lane_batch", -1);
+    tt.N = (int)t.number("num_samples", -1);
+    out.push_back(std::move(tt));
+  }
+  c->tunes = std::move(out);
   c->plan_B = -1;                                   // re-plan on the next call
   c->lanes.clear();
   return SDDM_OK;

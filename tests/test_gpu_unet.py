@@ -233,20 +233,32 @@ def test_transitions_match_reference(torch_cuda):
     print("worst transition diff", worst)
 
 
+_CONFIG5_ROWS = {}
+
+
+def config5_rows():
+    """4 rows of the config #5 chunk length (N=32832) at mixed noise levels and the numpy oracle's
+    fp32 forward of them."""
+    if not _CONFIG5_ROWS:
+        from oracle import unet
+        from sddm_hip.synth import noisy_speech
+        from _helpers import unet_arch
+        N, B = 32832, 4
+        rng = np.random.default_rng(12)
+        cond = noisy_speech(B, N, seed=12)
+        x_t = (0.7 * cond + 0.7 * rng.standard_normal(cond.shape)).astype(np.float32)
+        nl = np.array([0.99, 0.7, 0.4, 0.1], dtype=np.float32).reshape(B, 1, 1)
+        _CONFIG5_ROWS["rows"] = (cond, x_t, nl, unet.forward(unet_params(N), unet_arch(N), cond, x_t, nl.reshape(-1)))
+    return _CONFIG5_ROWS["rows"]
+
+
 @pytest.mark.parametrize("dtype,tol", [("float32", 1e-4), ("float16", 5e-3)])
 def test_unet_forward_config5_geometry(torch_cuda, dtype, tol):
     """BASELINE config #5 shape: 2.05 s chunks (N=32832, 512 frames; every level twice as tall)
     in fp16 storage with fp32 GroupNorm statistics, against the numpy oracle, B=4 with mixed
     noise levels (parity unpinned by a reference golden at this length: oracle only)."""
-    from oracle import unet
-    from sddm_hip.synth import noisy_speech
-    from _helpers import unet_arch
     N, B = 32832, 4
-    rng = np.random.default_rng(12)
-    cond = noisy_speech(B, N, seed=12)
-    x_t = (0.7 * cond + 0.7 * rng.standard_normal(cond.shape)).astype(np.float32)
-    nl = np.array([0.99, 0.7, 0.4, 0.1], dtype=np.float32).reshape(B, 1, 1)
-    ref = unet.forward(unet_params(N), unet_arch(N), cond, x_t, nl.reshape(-1))
+    cond, x_t, nl, ref = config5_rows()
     dev = torch_cuda.device("cuda", 0)
     eps = torch_cuda.full((B, 1, N), float("nan"), device=dev)
     make_ctx(N, dtype).network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
@@ -257,6 +269,50 @@ def test_unet_forward_config5_geometry(torch_cuda, dtype, tol):
     err = rms(got, ref)
     print(f"{dtype} forward N={N}: rms err {err:.3e}")
     assert err <= tol
+
+
+def test_unet_forward_config5_measured_table(torch_cuda):
+    """The repository's tuning file holds one table per measured geometry ({"tables": [...]}); a
+    config #5 plan (64-row lanes, N=32832, fp16) takes the config #5 table -- every conv runs the
+    kernel that table names, checked on the profiled op names -- and reproduces the oracle."""
+    import json
+    import os
+    N, B = 32832, 4
+    path = os.path.join(os.path.dirname(sddm_hip.__file__), "..", "configs", "conv_tuning.json")
+    text = open(path).read()
+    tabs = [t for t in json.loads(text).get("tables", []) if t["num_samples"] == N and t["lane_batch"] == 64]
+    if not tabs:
+        pytest.skip("no config #5 table in the repository")
+    want = tabs[0]["kernel"]
+    cond, x_t, nl, ref = config5_rows()
+    cfg = unet_config(N)
+    cfg["lane_rows"] = 64
+    ctx = sddm_hip.Context(cfg, 0, "float16")
+    for k, v in unet_params(N).items():
+        ctx.load_param("noise_estimate_model." + k, v)
+    ctx.set_conv_tuning(text)
+    dev = torch_cuda.device("cuda", 0)
+    eps = torch_cuda.full((B, 1, N), float("nan"), device=dev)
+    ctx.profile(True)
+    ctx.network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
+                        torch_cuda.from_numpy(nl).to(dev), eps)
+    torch_cuda.cuda.synchronize()
+    ops = ctx.profile_ops()
+    ctx.profile(False)
+    got = {}
+    for o in ops:
+        name, _, tag = o["name"].partition("[")
+        if tag:
+            tag = tag.rstrip("]")
+            got[name] = "strip" if tag == "strip" else (
+                "tile:" + tag[4:] if tag.startswith("tile") else "deep:" + tag[4:].replace("_", ":"))
+    for layer, k in want.items():
+        assert got.get(layer) == k, f"{layer}: table names {k}, plan ran {got.get(layer)}"
+    out = eps.cpu().numpy()
+    assert np.isfinite(out).all()
+    err = rms(out, ref)
+    print(f"config #5 table, fp16 forward N={N}: rms err {err:.3e}")
+    assert err <= 5e-3
 
 
 def test_multilane_graph_replay_equals_row_blocks(torch_cuda, monkeypatch):

@@ -39,7 +39,8 @@ if len(sys.argv) > 2:       # write the per-layer table for sddm_set_conv_tuning
         del kern["downs.0"]
     kern.pop("final_conv", None)
     lane_batch = int(os.environ.get("SWEEP_LANE_BATCH", "16"))
-    out = {"lane_batch": lane_batch, "dtype": "bfloat16", "num_samples": 16448,
+    out = {"lane_batch": lane_batch, "dtype": os.environ.get("SWEEP_DTYPE", "bfloat16"),
+           "num_samples": int(os.environ.get("SWEEP_NUM_SAMPLES", "16448")),
            "source": "tools/gpu_tile_sweep.sh + tools/sweep_merge.py (fastest measured kernel per layer)",
            "kernel": kern}
     json.dump(out, open(sys.argv[2], "w"), indent=1)
