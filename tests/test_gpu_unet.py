@@ -119,14 +119,20 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
         ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N,
                              "kernel": _TUNING if tuned == "table" else _TUNING16})
     elif tuned == "repo":
-        path = os.path.join(os.path.dirname(sddm_hip.__file__), "..", "configs", "conv_tuning.json")
-        if not os.path.exists(path):
+        text, tab = repo_tuning_table(N, B)
+        if tab is None:
             pytest.skip("no measured per-layer table in the repository")
-        ctx.set_conv_tuning(open(path).read())
+        ctx.set_conv_tuning(text)
+        ctx.profile(True)
     eps = torch_cuda.full((B, 1, N), float("nan"), device=dev)
     ctx.network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
                         torch_cuda.from_numpy(nl).to(dev), eps)
     torch_cuda.cuda.synchronize()
+    if tuned == "repo":     # the headline table is the one the plan took (the file holds several)
+        got = planned_kernels(ctx)
+        ctx.profile(False)
+        for layer, k in tab["kernel"].items():
+            assert got.get(layer) == k, f"{layer}: table names {k}, plan ran {got.get(layer)}"
     eps = eps.cpu().numpy()
     errs = [rms(eps[b], ref[b]) for b in range(B)]
     print(f"{dtype} {tuned} B={B} forward: row rms min {min(errs):.3e} max {max(errs):.3e} (ref rms {rms(ref, 0):.3f})")
@@ -233,6 +239,32 @@ def test_transitions_match_reference(torch_cuda):
     print("worst transition diff", worst)
 
 
+def planned_kernels(ctx):
+    """{layer: "strip" | "tile:<cfg>" | "deep:<mt>:<nw>:<nb>"} of the last profiled call (the
+    tuning table's vocabulary, parsed from the profiled op names)."""
+    got = {}
+    for o in ctx.profile_ops():
+        name, _, tag = o["name"].partition("[")
+        if tag:
+            tag = tag.rstrip("]")
+            got[name] = "strip" if tag == "strip" else (
+                "tile:" + tag[4:] if tag.startswith("tile") else "deep:" + tag[4:].replace("_", ":"))
+    return got
+
+
+def repo_tuning_table(N, lane_batch):
+    """(file text, the table for this geometry) of the repository's tuning file, or (None, None)."""
+    import json
+    import os
+    path = os.path.join(os.path.dirname(sddm_hip.__file__), "..", "configs", "conv_tuning.json")
+    if not os.path.exists(path):
+        return None, None
+    text = open(path).read()
+    j = json.loads(text)
+    tabs = [t for t in j.get("tables", [j]) if t["num_samples"] == N and t["lane_batch"] == lane_batch]
+    return text, (tabs[0] if tabs else None)
+
+
 _CONFIG5_ROWS = {}
 
 
@@ -275,15 +307,11 @@ def test_unet_forward_config5_measured_table(torch_cuda):
     """The repository's tuning file holds one table per measured geometry ({"tables": [...]}); a
     config #5 plan (64-row lanes, N=32832, fp16) takes the config #5 table -- every conv runs the
     kernel that table names, checked on the profiled op names -- and reproduces the oracle."""
-    import json
-    import os
     N, B = 32832, 4
-    path = os.path.join(os.path.dirname(sddm_hip.__file__), "..", "configs", "conv_tuning.json")
-    text = open(path).read()
-    tabs = [t for t in json.loads(text).get("tables", []) if t["num_samples"] == N and t["lane_batch"] == 64]
-    if not tabs:
+    text, tab = repo_tuning_table(N, 64)
+    if tab is None:
         pytest.skip("no config #5 table in the repository")
-    want = tabs[0]["kernel"]
+    want = tab["kernel"]
     cond, x_t, nl, ref = config5_rows()
     cfg = unet_config(N)
     cfg["lane_rows"] = 64
@@ -297,15 +325,8 @@ def test_unet_forward_config5_measured_table(torch_cuda):
     ctx.network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
                         torch_cuda.from_numpy(nl).to(dev), eps)
     torch_cuda.cuda.synchronize()
-    ops = ctx.profile_ops()
+    got = planned_kernels(ctx)
     ctx.profile(False)
-    got = {}
-    for o in ops:
-        name, _, tag = o["name"].partition("[")
-        if tag:
-            tag = tag.rstrip("]")
-            got[name] = "strip" if tag == "strip" else (
-                "tile:" + tag[4:] if tag.startswith("tile") else "deep:" + tag[4:].replace("_", ":"))
     for layer, k in want.items():
         assert got.get(layer) == k, f"{layer}: table names {k}, plan ran {got.get(layer)}"
     out = eps.cpu().numpy()
