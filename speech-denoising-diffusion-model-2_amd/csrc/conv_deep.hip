@@ -126,6 +126,16 @@ static constexpr ConvShape kDeepShapes[] = {
     {128, 0, 8, 16, 32, 16, 96, 0, 96, 128, 128, 2, 1, 0, 8, 32},        // ups.5.block2
     {128, 0, 8, 16, 32, 16, 96, 96, 96, 0, 0, 0, 1, 0, 8, 32},           // ups.6.block1
     {128, 0, 8, 16, 32, 16, 96, 0, 96, 96, 96, 2, 1, 0, 4, 32},          // ups.6.block2
+    // BASELINE config #5 per GPU (32832 samples, 64-row lanes, fp16) with its measured table
+    {64, 1, 4, 16, 64, 16, 96, 0, 96, 0, 0, 0, 0, 0, 4, 32, 1},          // c5:downs.6
+    {64, 0, 8, 8, 32, 8, 128, 0, 160, 0, 0, 0, 1, 0, 4, 32, 1},          // c5:downs.9.block1
+    {64, 0, 8, 8, 32, 8, 160, 0, 160, 128, 0, 2, 1, 0, 4, 32, 1},        // c5:downs.9.block2
+    {32, 1, 8, 4, 16, 4, 160, 0, 160, 0, 0, 0, 0, 0, 4, 32, 1},          // c5:downs.10
+    {32, 0, 8, 4, 16, 4, 160, 0, 160, 0, 0, 0, 1, 0, 4, 32, 1},          // c5:mid.0.block1
+    {32, 0, 8, 4, 16, 4, 160, 0, 160, 0, 0, 1, 1, 0, 4, 32, 1},          // c5:mid.0.block2
+    {32, 0, 8, 4, 16, 4, 160, 160, 160, 0, 0, 0, 1, 0, 4, 32, 1},        // c5:ups.0.block1
+    {32, 0, 8, 4, 16, 4, 160, 0, 160, 160, 160, 2, 1, 0, 4, 32, 1},      // c5:ups.0.block2
+    {64, 0, 8, 8, 32, 8, 160, 0, 160, 0, 0, 0, 0, 1, 4, 32, 1},          // c5:ups.1
 };
 static constexpr int kNDeepShapes = (int)(sizeof(kDeepShapes) / sizeof(kDeepShapes[0]));
 
@@ -502,6 +512,8 @@ template <typename T, int SH>
 static bool deep_shape_go(int mt, int nw, int nb, bool s2, const ConvArgs& a, int B, hipStream_t s, hipError_t& e) {
   if constexpr (SH >= kNDeepShapes || sizeof(T) == 4) {
     return false;
+  } else if constexpr (!shape_for_type<T>(kDeepShapes[SH])) {
+    return deep_shape_go<T, SH + 1>(mt, nw, nb, s2, a, B, s, e);
   } else {
     constexpr ConvShape c = kDeepShapes[SH];
     if (c.cfg == mt && c.nw == nw && c.nb == nb && conv_shape_geo_matches(c, s2, a)) {

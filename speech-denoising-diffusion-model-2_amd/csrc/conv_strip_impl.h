@@ -66,6 +66,18 @@ static constexpr ConvShape kStripShapes[] = {
     {32, 0, 16, 128, 256, 128, 32, 0, 32, 0, 0, 0, 0, 1, 256, 16},      // ups.13 (Upsample)
     {32, 0, 16, 128, 256, 128, 32, 32, 32, 0, 0, 0, 1, 0, 256, 16},     // ups.14.block1
     {32, 0, 16, 128, 256, 128, 32, 0, 32, 32, 32, 2, 1, 0, 256, 16},    // ups.14.block2
+    // BASELINE config #5 per GPU (32832 samples, 64-row lanes, fp16) with its measured table
+    {32, 0, 64, 128, 512, 128, 32, 0, 32, 0, 0, 0, 1, 0, 256, 64, 1},   // c5:downs.1.block1
+    {32, 0, 64, 128, 512, 128, 32, 0, 32, 0, 0, 1, 1, 0, 256, 64, 1},   // c5:downs.1.block2
+    {64, 0, 64, 64, 256, 64, 32, 0, 64, 0, 0, 0, 1, 0, 256, 64, 1},     // c5:downs.3.block1
+    {32, 0, 128, 64, 256, 64, 64, 0, 64, 32, 0, 2, 1, 0, 256, 128, 1},  // c5:downs.3.block2
+    {32, 0, 128, 64, 256, 64, 64, 0, 64, 0, 0, 0, 0, 1, 256, 128, 1},   // c5:ups.10
+    {32, 0, 64, 64, 256, 64, 32, 0, 32, 64, 64, 2, 1, 0, 256, 64, 1},   // c5:ups.11.block2
+    {32, 0, 64, 64, 256, 64, 32, 32, 32, 0, 0, 0, 1, 0, 256, 64, 1},    // c5:ups.12.block1
+    {32, 0, 64, 64, 256, 64, 32, 0, 32, 32, 32, 2, 1, 0, 256, 64, 1},   // c5:ups.12.block2
+    {32, 0, 64, 128, 512, 128, 32, 0, 32, 0, 0, 0, 0, 1, 256, 64, 1},   // c5:ups.13
+    {32, 0, 64, 128, 512, 128, 32, 32, 32, 0, 0, 0, 1, 0, 256, 64, 1},  // c5:ups.14.block1
+    {32, 0, 64, 128, 512, 128, 32, 0, 32, 32, 32, 2, 1, 0, 256, 64, 1}, // c5:ups.14.block2
 };
 static constexpr int kNStripShapes = (int)(sizeof(kStripShapes) / sizeof(kStripShapes[0]));
 
@@ -559,6 +571,8 @@ template <typename T, int SH>
 static bool strip_shape_go(const ConvArgs& a, int nblk, int mpi, int SR, int B, hipStream_t s, hipError_t& e) {
   if constexpr (SH >= kNStripShapes || sizeof(T) == 4) {
     return false;
+  } else if constexpr (!shape_for_type<T>(kStripShapes[SH])) {
+    return strip_shape_go<T, SH + 1>(a, nblk, mpi, SR, B, s, e);
   } else {
     constexpr ConvShape c = kStripShapes[SH];
     if (strip_shape_matches(c, nblk, mpi, SR, a)) {

@@ -424,7 +424,7 @@ static bool tile_shape_go(int cfg, const ConvArgs& a, int B, hipStream_t s, hipE
     return false;
   } else {
     constexpr ConvShape c = kTileShapes[SH];
-    if constexpr (c.s2 == (S2 ? 1 : 0)) {
+    if constexpr (c.s2 == (S2 ? 1 : 0) && shape_for_type<T>(c)) {
       if (c.cfg == cfg && conv_shape_geo_matches(c, S2, a)) { e = tile_go<T, S2, c.cfg, SH>(a, B, s); return true; }
     }
     return tile_shape_go<T, S2, SH + 1>(cfg, a, B, s, e);

@@ -1,5 +1,6 @@
 // Tile configurations and LDS geometry of the K-streamed tile kernel (conv_tile.hip).
 #pragma once
+#include <type_traits>
 #include "conv_common.h"
 #include "kernels.h"
 
@@ -34,7 +35,14 @@ static constexpr int kNTileCfgs = (int)(sizeof(kTileCfgs) / sizeof(kTileCfgs[0])
 // the launch, so other configurations and signal lengths run the generic kernel.  Constant
 // geometry folds the index arithmetic of every staging unit, tap and output pixel: the
 // downs.2 tile kernel drops from ~5000 to ~1200 instructions and from 25 to 18 us.
-struct ConvShape { int cfg, s2, TR, TW, Ho, Wo, CA, CB, Cout, RCA, RCB, res, gn, up, nw, nb; };
+// f16only: the row is instantiated for fp16 storage only (the config #5 rows: BASELINE config #5
+// runs in fp16), otherwise for both 16-bit types
+struct ConvShape { int cfg, s2, TR, TW, Ho, Wo, CA, CB, Cout, RCA, RCB, res, gn, up, nw, nb, f16only; };
+
+// a shape row applies to storage type T
+template <typename T> __host__ __device__ constexpr bool shape_for_type(const ConvShape& c) {
+  return sizeof(T) == 2 && (!c.f16only || std::is_same<T, f16_t>::value);
+}
 
 __host__ inline bool conv_shape_geo_matches(const ConvShape& c, bool s2, const ConvArgs& a) {
   return c.s2 == (s2 ? 1 : 0) && c.TR == a.TR && c.TW == a.TW && c.Ho == a.Ho && c.Wo == a.Wo &&
@@ -68,6 +76,29 @@ static constexpr ConvShape kTileShapes[] = {
     {1, 0, 8, 32, 64, 32, 64, 64, 64, 0, 0, 0, 1, 0},          // ups.9.block1
     {2, 0, 4, 32, 64, 32, 64, 0, 64, 64, 64, 2, 1, 0},         // ups.9.block2
     {12, 0, 8, 64, 128, 64, 64, 64, 32, 0, 0, 0, 1, 0},        // ups.11.block1
+    // BASELINE config #5 per GPU (32832 samples, 64-row lanes, fp16) with its measured table
+    {4, 1, 2, 64, 256, 64, 32, 0, 32, 0, 0, 0, 0, 0, 0, 0, 1},          // c5:downs.2
+    {2, 1, 4, 32, 128, 32, 64, 0, 64, 0, 0, 0, 0, 0, 0, 0, 1},          // c5:downs.4
+    {3, 0, 8, 32, 128, 32, 64, 0, 96, 0, 0, 0, 1, 0, 0, 0, 1},          // c5:downs.5.block1
+    {3, 0, 8, 32, 128, 32, 96, 0, 96, 64, 0, 2, 1, 0, 0, 0, 1},         // c5:downs.5.block2
+    {0, 0, 16, 16, 64, 16, 96, 0, 128, 0, 0, 0, 1, 0, 0, 0, 1},         // c5:downs.7.block1
+    {0, 0, 16, 16, 64, 16, 128, 0, 128, 96, 0, 2, 1, 0, 0, 0, 1},       // c5:downs.7.block2
+    {2, 1, 16, 8, 32, 8, 128, 0, 128, 0, 0, 0, 0, 0, 0, 0, 1},          // c5:downs.8
+    {2, 0, 16, 8, 32, 8, 160, 160, 128, 0, 0, 0, 1, 0, 0, 0, 1},        // c5:ups.2.block1
+    {2, 0, 16, 8, 32, 8, 128, 0, 128, 160, 160, 2, 1, 0, 0, 0, 1},      // c5:ups.2.block2
+    {2, 0, 16, 8, 32, 8, 128, 128, 128, 0, 0, 0, 1, 0, 0, 0, 1},        // c5:ups.3.block1
+    {2, 0, 16, 8, 32, 8, 128, 0, 128, 128, 128, 2, 1, 0, 0, 0, 1},      // c5:ups.3.block2
+    {0, 0, 16, 16, 64, 16, 128, 0, 128, 0, 0, 0, 0, 1, 0, 0, 1},        // c5:ups.4
+    {3, 0, 16, 16, 64, 16, 128, 128, 96, 0, 0, 0, 1, 0, 0, 0, 1},       // c5:ups.5.block1
+    {3, 0, 16, 16, 64, 16, 96, 0, 96, 128, 128, 2, 1, 0, 0, 0, 1},      // c5:ups.5.block2
+    {3, 0, 16, 16, 64, 16, 96, 96, 96, 0, 0, 0, 1, 0, 0, 0, 1},         // c5:ups.6.block1
+    {3, 0, 16, 16, 64, 16, 96, 0, 96, 96, 96, 2, 1, 0, 0, 0, 1},        // c5:ups.6.block2
+    {3, 0, 8, 32, 128, 32, 96, 0, 96, 0, 0, 0, 0, 1, 0, 0, 1},          // c5:ups.7
+    {0, 0, 8, 32, 128, 32, 96, 96, 64, 0, 0, 0, 1, 0, 0, 0, 1},         // c5:ups.8.block1
+    {0, 0, 8, 32, 128, 32, 64, 0, 64, 96, 96, 2, 1, 0, 0, 0, 1},        // c5:ups.8.block2
+    {0, 0, 8, 32, 128, 32, 64, 64, 64, 0, 0, 0, 1, 0, 0, 0, 1},         // c5:ups.9.block1
+    {0, 0, 8, 32, 128, 32, 64, 0, 64, 64, 64, 2, 1, 0, 0, 0, 1},        // c5:ups.9.block2
+    {12, 0, 8, 64, 256, 64, 64, 64, 32, 0, 0, 0, 1, 0, 0, 0, 1},        // c5:ups.11.block1
 };
 static constexpr int kNTileShapes = (int)(sizeof(kTileShapes) / sizeof(kTileShapes[0]));
 

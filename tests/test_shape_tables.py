@@ -1,6 +1,6 @@
 """CPU: the compile-time layer-shape tables (conv_tile_cfg.h kTileShapes, conv_deep.hip kDeepShapes,
 conv_strip_impl.h kStripShapes; DESIGN.md §3 "Compile-time layer shapes") agree with the measured
-per-layer kernel table (configs/conv_tuning.json) and cover every conv of the headline plan.  A
+per-layer kernel tables (configs/conv_tuning.json) and cover every conv of the headline and config #5 plans.  A
 row that drifts from the table is never wrong (the launch falls back to the generic kernel when a
 field differs) but silently loses the specialisation, so the drift is caught here."""
 import json
@@ -10,7 +10,8 @@ import re
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(REPO, "speech-denoising-diffusion-model-2_amd", "csrc")
 TUNING = os.path.join(REPO, "speech-denoising-diffusion-model-2_amd", "configs", "conv_tuning.json")
-FIELDS = ("cfg", "s2", "TR", "TW", "Ho", "Wo", "CA", "CB", "Cout", "RCA", "RCB", "res", "gn", "up", "nw", "nb")
+FIELDS = ("cfg", "s2", "TR", "TW", "Ho", "Wo", "CA", "CB", "Cout", "RCA", "RCB", "res", "gn", "up", "nw", "nb",
+          "f16only")
 
 
 def _rows(path, table):
@@ -35,20 +36,37 @@ def test_generic_entry_first():
         assert rows[0][0] == "generic" and rows[0][1]["cfg"] == -1, kind
 
 
-def _headline_table():
-    """The table measured for the headline geometry (the file holds one table or {"tables": [...]})."""
+# row name prefix -> (num_samples, lane_batch) of the measured table the rows encode
+GEOMETRIES = {"": (16448, 16), "c5:": (32832, 64)}
+
+
+def _table(prefix):
+    """The measured table of one geometry (the file holds one table or {"tables": [...]})."""
     tuning = json.load(open(TUNING))
     tabs = tuning["tables"] if "tables" in tuning else [tuning]
-    heads = [t for t in tabs if t["num_samples"] == 16448 and t["lane_batch"] == 16]   # the geometry the rows encode
-    assert len(heads) == 1
-    return heads[0]
+    n, lb = GEOMETRIES[prefix]
+    hits = [t for t in tabs if t["num_samples"] == n and t["lane_batch"] == lb]
+    assert len(hits) == 1
+    return hits[0]
+
+
+def _headline_table():
+    return _table("")
+
+
+def _split(name):
+    """(geometry prefix, layer name) of a shape row's name."""
+    return ("c5:", name[3:]) if name.startswith("c5:") else ("", name)
 
 
 def test_rows_match_the_measured_kernel_table():
-    kern = _headline_table()["kernel"]
     for kind, rows in _tables().items():
-        for name, r in rows[1:]:
-            assert name in kern, f"{kind} shape row {name} names no layer of the tuning table"
+        for full, r in rows[1:]:
+            prefix, name = _split(full)
+            kern = _table(prefix)["kernel"]
+            assert name in kern, f"{kind} shape row {full} names no layer of the tuning table"
+            # the config #5 rows are instantiated for fp16 only (its configured dtype)
+            assert r["f16only"] == (1 if prefix else 0), full
             if kind == "tile":
                 want = f"tile:{r['cfg']}"
             elif kind == "deep":
@@ -59,9 +77,10 @@ def test_rows_match_the_measured_kernel_table():
 
 
 def test_every_tuned_layer_has_exactly_one_shape():
-    kern = _headline_table()["kernel"]
-    names = [n for rows in _tables().values() for n, _ in rows[1:]]
-    assert sorted(names) == sorted(kern), set(names) ^ set(kern)
+    for prefix in GEOMETRIES:
+        kern = _table(prefix)["kernel"]
+        names = [_split(n)[1] for rows in _tables().values() for n, _ in rows[1:] if _split(n)[0] == prefix]
+        assert sorted(names) == sorted(kern), (prefix, set(names) ^ set(kern))
 
 
 def test_row_invariants():
