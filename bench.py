@@ -11,6 +11,11 @@ outputs are all-gathered over RCCL at the end of the step (weak scaling).
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--timesteps T] [--dtype bf16]
     python bench.py --workload diffwave|wavegrad     # BASELINE configs #3 / #4 (not the headline)
 
+At N=1 the headline line also carries `variants`: the fp32 parity path (2 timed runs) and the other
+16-bit type (fp16 beside the bf16 headline, 5 timed runs), timed in the same process on the same
+workload after the headline's timed region, each with the RMS drift of its output from the fp32
+output of the same seed (`drift_vs_f32_rms`; north_star's bar is 1e-3).
+
 Rank 0 prints one JSON line.  `roofline` is the dominant kernel's (the template instantiation with
 the most time in a sampling run): algorithmic bytes per launch over its average duration, from HIP
 events around every launch of one extra (untimed) sampling run, with the whole reverse step
@@ -150,7 +155,8 @@ def kernel_src_hash():
     return h.hexdigest()[:16]
 
 
-TRAFFIC_FILES = ("r05_hbm_traffic.json", "r05_config5_hbm_traffic.json", "r04_hbm_traffic.json",
+TRAFFIC_FILES = ("r06_hbm_traffic.json", "r06_f16_hbm_traffic.json", "r06_config5_hbm_traffic.json",
+                 "r05_hbm_traffic.json", "r05_config5_hbm_traffic.json", "r04_hbm_traffic.json",
                  "r04_config5_hbm_traffic.json")   # newest first
 
 
@@ -229,6 +235,41 @@ def unet_roofline(model, cond, N, B, T, dtype, ms_per_run):
                      "frac": round(step_bytes / (step_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                      "mfma_tflops": round(step_flops / (step_ms * 1e-3) / 1e12, 2),
                      "launches": len(ops), "launch_time_ms": round(total_ms / T, 5)}}
+
+
+DTYPE_NAMES = {"bf16": "bfloat16", "f16": "float16", "f32": "float32"}
+
+
+def rms(a, b):
+    """RMS difference of two sampled batches (tests/_helpers.py rms: the drift DESIGN.md §4 quotes)"""
+    import torch
+    return float(torch.sqrt(torch.mean((a.double() - b.double()) ** 2)).item())
+
+
+def unet_variant(model, step, result, dtype, steps, warmup, N, B, T, cond_all, no_profile):
+    """A precision sub-record of the headline line, timed in the same process on the same workload
+    (same condition, seed and weights; the library packs the weights in `dtype`): W untimed runs, K
+    timed runs bracketed by torch.cuda.synchronize(), the same roofline fields as the headline."""
+    import torch
+    model.compute_dtype = DTYPE_NAMES[dtype]
+    log(f"{dtype} sub-record: {warmup} warmup + {steps} timed sampling runs")
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out = result["out"].clone()
+    if not torch.isfinite(out).all():
+        raise RuntimeError(f"non-finite samples ({dtype})")
+    v = {"value": round(steps * B * N / 16000.0 / el, 4), "unit": "audio_s/s", "steps": steps, "warmup": warmup,
+         "ms_per_step": round(1e3 * el / steps, 3), "dtype": dtype}
+    if not no_profile:
+        v["roofline"] = unet_roofline(model, cond_all[:B].contiguous(), N, B, T, dtype, 1e3 * el / steps)
+    v["out"] = out
+    return v
 
 
 # spectrogram-conditioned workloads (BASELINE.json configs #3 and #4): config, frames, clips per GPU,
@@ -378,6 +419,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=3, help="CPU reverse steps at the config's batch (extrapolated x T)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-variants", action="store_true", help="skip the same-run fp16 / fp32 sub-records")
+    ap.add_argument("--f16-steps", type=int, default=5, help="timed runs of the 16-bit sub-record")
+    ap.add_argument("--f32-steps", type=int, default=2, help="timed runs of the fp32 sub-record")
     ap.add_argument("--workload", default="unet", choices=["unet", "diffwave", "wavegrad"])
     ap.add_argument("--num-samples", type=int, default=None,
                     help="UNet chunk length (config #5: 32832 = 512 frames); default config_unet.json's 16448")
@@ -411,8 +455,8 @@ def main():
     diffusion = config.init_obj("diffusion", module_diffusion, device=dev)
     network = config.init_obj("network", module_network, num_samples=N)
     model = config.init_obj("arch", module_arch, diffusion, network).to(dev).eval()
-    model.compute_dtype = {"bf16": "bfloat16", "f16": "float16", "f32": "float32"}[args.dtype]
-    model.lane_rows = 64 if B >= 64 else None                      # 64-row lanes for large per-GPU batches
+    model.compute_dtype = DTYPE_NAMES[args.dtype]
+    model.lane_rows = 64 if B >= 64 else None                     # 64-row lanes for large per-GPU batches
 
     cond_all = torch.from_numpy(noisy_speech(B * world, N, seed=1234)).to(dev)   # VoiceBank-DEMAND-shaped chunks
     result = {}
@@ -449,6 +493,24 @@ def main():
         log("profiling one sampling run (HIP events around every launch)")
         roofline = unet_roofline(model, cond_all[:B].contiguous(), N, B, T, args.dtype, 1e3 * elapsed / args.steps)
 
+    # same-run precision sub-records (N=1 only, after the timed region): the fp32 parity path and the
+    # fp16 twin of the headline, each timed on the same workload, with the RMS drift of every
+    # 16-bit output from the fp32 output of the same seed (north_star's bar: 1e-3)
+    variants = None
+    if (world == 1 and rank == 0 and not args.no_variants and args.dtype != "f32" and B <= 16
+            and not args.num_samples):                             # the headline workload only
+        main_out, main_dtype = result["out"], model.compute_dtype
+        variants = {}
+        v32 = unet_variant(model, step, result, "f32", args.f32_steps, 1, N, B, T, cond_all, args.no_profile)
+        out32 = v32.pop("out")
+        for dt in [d for d in ("f16", "bf16") if d != args.dtype]:
+            v = unet_variant(model, step, result, dt, args.f16_steps, 1, N, B, T, cond_all, args.no_profile)
+            v["drift_vs_f32_rms"] = rms(v.pop("out"), out32)
+            variants[dt] = v
+        variants["f32"] = v32
+        drift_main = rms(main_out, out32)
+        model.compute_dtype = main_dtype
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:   # CPU baseline: rank 0 at N=1 only
         log("CPU baseline")
@@ -477,6 +539,9 @@ def main():
                            "model": "UNetModified2", "global_batch": B * world, "seq_len": N,
                            "timesteps": T, "parallelism": f"dp{world}", "lane_rows": model.lane_rows or 16},
                 "roofline": roofline, "cpu_baseline": cpu}
+        if variants is not None:
+            line["drift_vs_f32_rms"] = drift_main
+            line["variants"] = variants
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -120,9 +120,9 @@ int sddm_q_sample(sddm_ctx* ctx, int mode, const float* x0, const float* y, cons
 /* Measured per-layer conv kernels (no reference counterpart: a tuning table).  json = one table
  * {"lane_batch": B, "dtype": "bfloat16", "num_samples": N, "kernel": {"<layer name>": "strip" |
  * "tile:<cfg>" | "deep:<pixels>:<waves>:<channels>", ...}} or {"tables": [table, ...]}; at the next
- * plan build the first table whose lane batch / dtype / num_samples match the plan applies (a
- * bfloat16 table also serves float16), none otherwise (and per layer whenever the requested
- * kernel does not fit that layer). */
+ * plan build the first table whose lane batch / dtype / num_samples match the plan applies; a
+ * float16 plan with no float16 table takes a matching bfloat16 one (never the reverse); none
+ * otherwise (and per layer whenever the requested kernel does not fit that layer). */
 int sddm_set_conv_tuning(sddm_ctx* ctx, const char* json);
 
 /* Replaces the torchaudio featurizer of prepare_spectrogram.py:20-55 (context-free):

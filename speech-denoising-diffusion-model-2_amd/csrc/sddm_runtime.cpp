@@ -704,12 +704,15 @@ static int build_lane(sddm_ctx* c, Lane& L) {
   // every lane, and every row partition of a batch (sharded runs), gets the same kernels, tiles
   // and GroupNorm tilings, hence bit-identical rows
   const int PB = std::max(1, c->lane_rows);
-  // (a table measured in bf16 also serves f16: the same kernels at the same bytes and MFMA rate)
+  // A table measured for this exact dtype wins; failing that, a bfloat16 table also serves float16
+  // (the same kernels at the same bytes and MFMA rate).  Never the other way: the float16 rows
+  // (config #5) have fp16-only compile-time shapes (ConvShape::f16only).
   const sddm_ctx::TuneTable* tuned = nullptr;
-  for (const auto& tt : c->tunes) {
-    const bool same_dt = tt.dtype == dt || (tt.dtype >= 0 && tt.dtype != DT_F32 && dt != DT_F32);
-    if (tt.B == PB && same_dt && tt.N == N) { tuned = &tt; break; }
-  }
+  for (const auto& tt : c->tunes)
+    if (tt.B == PB && tt.N == N && tt.dtype == dt) { tuned = &tt; break; }
+  if (!tuned && dt == DT_F16)
+    for (const auto& tt : c->tunes)
+      if (tt.B == PB && tt.N == N && tt.dtype == DT_BF16) { tuned = &tt; break; }
   auto pick = [&](const std::string& name, int Cin, int RC, int res_mode, int Ho, int Wo, int cout, bool s2, bool up,
                   ConvChoice& ch) {
     int wm = 0, wn = 0, wb = 0, kind = 0, ka = 0;

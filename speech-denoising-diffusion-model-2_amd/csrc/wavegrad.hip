@@ -63,10 +63,16 @@ template <typename T> __device__ __forceinline__ Frag<T> zero_frag() {
   return pack8<T>(z);
 }
 
-// (0 <= t < 2^21: t / f through the float reciprocal, exact by fdivi's margin, instead of an
-// integer division sequence per staged element; the reciprocal of the uniform f is hoisted)
+// t / f through the float reciprocal instead of an integer division sequence per staged element
+// (the reciprocal of the uniform f is hoisted): fdivi is exact for 0 <= t < 2^21, and one
+// correction step each way keeps the quotient exact while the float estimate is off by at most
+// one, i.e. for every t < 2^23 (launch_wg_conv rejects longer signals)
 __device__ __forceinline__ int wg_map(int t, int map, int f) {
-  return map == WG_MAP_UP ? fdivi(t, 1.0f / (float)f) : (map == WG_MAP_DOWN ? t * f : t);
+  if (map != WG_MAP_UP) return map == WG_MAP_DOWN ? t * f : t;
+  int q = fdivi(t, 1.0f / (float)f);
+  q -= q * f > t ? 1 : 0;
+  q += (q + 1) * f <= t ? 1 : 0;
+  return q;
 }
 
 // epilogue FiLM of the next conv's input (wavegrad.py:98-99, 104-105, 107-108): m = leaky(shift +
@@ -501,6 +507,8 @@ hipError_t launch_wg_conv(int dtype, const WGConvArgs& a, hipStream_t s) {
   if (a.post_film && (a.post_film > 2 || !a.efilm || a.out_f32 || a.Cout % 4 || (a.post_film == 2 && !a.out2)))
     return hipErrorInvalidValue;
   if (a.res && ((a.res_map == WG_MAP_UP && a.res_T * a.res_f != a.Tc) || (a.res_map == WG_MAP_ID && a.res_T != a.Tc)))
+    return hipErrorInvalidValue;
+  if (a.Tc >= kWgMaxPositions || a.src_T >= kWgMaxPositions)   // wg_map's exact range
     return hipErrorInvalidValue;
   const dim3 grid((a.Tc + WG_MT - 1) / WG_MT, (a.Cout + WG_MC - 1) / WG_MC, a.B);
   if (dtype == DT_F32) wg_conv_dispatch<float>(a, grid, s);

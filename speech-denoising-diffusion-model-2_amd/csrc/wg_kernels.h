@@ -13,6 +13,8 @@ namespace sddm {
 // post: 0 none | 1 leaky_relu(0.2) then + enc[row][co] (FiLM input_conv + PositionalEncoding).
 // res:  + res[b][rmap(t)][co] (DBlock residual_dense, UBlock block1 / x), rmap identity or up.
 enum { WG_MAP_ID = 0, WG_MAP_UP = 1, WG_MAP_DOWN = 2 };
+// positions per WaveGrad conv launch: the staging index map (wg_map) is exact below 2^23
+constexpr int kWgMaxPositions = 1 << 23;
 struct WGConvArgs {
   const void* src; int src_T, src_C, map, f;   // source [B][src_T][src_C] (T); channels [0, Cin) are read
   int Tc, Cin, K, dil, pre;

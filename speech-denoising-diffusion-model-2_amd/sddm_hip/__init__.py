@@ -114,7 +114,9 @@ class Context:
         check(lib().sddm_create(self.device, self.dtype, ctypes.byref(h)))
         self._h = h
         check(lib().sddm_configure(self._h, json.dumps(config).encode()))
-        self.timesteps = int(config.get("diffusion", {}).get("args", {}).get("n_timestep", 0)) or None
+        # the library's own default when the schedule names no n_timestep (sddm_configure: 1000), so
+        # sample_noise always checks the T + 1 draws it reads
+        self.timesteps = int(config.get("diffusion", {}).get("args", {}).get("n_timestep", 1000))
 
     def close(self):
         if getattr(self, "_h", None):
@@ -161,7 +163,7 @@ class Context:
             raise ValueError("noise must be a contiguous float32 tensor")
         if noise.device != out.device:
             raise ValueError(f"noise must be on {out.device}, got {noise.device}")
-        if noise.dim() < 2 or noise.shape[1] != B or (T is not None and noise.shape[0] != T + 1) or \
+        if noise.dim() < 2 or noise.shape[1] != B or noise.shape[0] != T + 1 or \
                 noise.numel() != noise.shape[0] * B * N:
             raise ValueError(f"noise must be [T + 1, {B}, {N}] draws, got {tuple(noise.shape)}")
         check(lib().sddm_sample_noise(self._h, _ptr(cond), B, N, _ptr(noise), _ptr(out), _stream(torch, cond.device)))

@@ -88,6 +88,22 @@ def test_reference_noise_layout_and_errors(torch_cuda):
         m.infer(cond.cuda(), noise=torch.zeros(3, 2, 1, N))
 
 
+def test_sample_noise_checks_default_timesteps(torch_cuda):
+    """A library config without n_timestep runs the library's default T = 1000 (sddm_configure), so
+    the Context checks a caller noise buffer against 1001 draws: a shorter one raises instead of
+    letting the library read past its end."""
+    import sddm_hip
+    from _helpers import unet_config
+    N = 2112
+    cfg = unet_config(N, ("linear", 4, 1e-4, 0.05))
+    del cfg["diffusion"]["args"]["n_timestep"]
+    ctx = sddm_hip.Context(cfg, 0, "float32")
+    assert ctx.timesteps == 1000
+    cond = torch.zeros(1, 1, N, device="cuda")
+    with pytest.raises(ValueError):
+        ctx.sample_noise(cond, torch.empty_like(cond), torch.zeros(5, 1, 1, N, device="cuda"))
+
+
 def test_unet_caller_noise_across_lanes(torch_cuda):
     """Caller noise with B larger than the lane (lane_rows = 2, B = 4: two lanes, each reading its rows
     of every draw at noise + row0 * N with stride B * N, final_kernel's vector noise loads included):

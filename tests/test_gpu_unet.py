@@ -99,11 +99,17 @@ _TUNING16 = {"downs.7.block1": "deep:64:8:16", "downs.7.block2": "deep:128:4:16"
              "ups.0.block2": "deep:16:4:16", "ups.1": "deep:64:4:16", "ups.4": "deep:128:8:16",
              "ups.5.block1": "deep:64:8:16", "ups.6.block2": "deep:128:4:16"}
 
+# producers of 32 tiles per image at 32x16 (16-pixel deep tiles): their consumers (downs.7.block2,
+# ups.5.block2) combine 128 / 96 (tile, channel) statistics per group, more than one GroupNorm load
+# round trip holds (64), so they take the fp64 two-pass finalize (gn_fused_prologue)
+_TUNING16_GN = {**_TUNING16, "downs.7.block1": "deep:16:4:16", "ups.5.block1": "deep:16:4:16",
+                "ups.5.block2": "deep:128:8:16"}
+
 
 @pytest.mark.parametrize("dtype,tol,tuned", [("float32", 1e-4, None), ("bfloat16", 2.5e-2, None),
                                             ("bfloat16", 2.5e-2, "table"), ("bfloat16", 2.5e-2, "repo"),
                                             ("bfloat16", 2.5e-2, "table16"), ("float32", 1e-4, "table16"),
-                                            ("float16", 5e-3, None)])
+                                            ("bfloat16", 2.5e-2, "table16gn"), ("float16", 5e-3, None)])
 def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     """B=16 x N=16448 (the bench shape), 16 distinct rows at 16 noise levels: the kernels and tiles
     picked for a full lane (and per-layer kernels set through sddm_set_conv_tuning: a table
@@ -114,10 +120,11 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     cond, x_t, nl, ref = bench_rows(N, B)
     dev = torch_cuda.device("cuda", 0)
     ctx = make_ctx(N, dtype)
-    if tuned in ("table", "table16"):
+    if tuned in ("table", "table16", "table16gn"):
         # per-layer kernels everywhere
         ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N,
-                             "kernel": _TUNING if tuned == "table" else _TUNING16})
+                             "kernel": {"table": _TUNING, "table16": _TUNING16, "table16gn": _TUNING16_GN}[tuned]})
+        ctx.profile(True)
     elif tuned == "repo":
         text, tab = repo_tuning_table(N, B)
         if tab is None:
@@ -133,6 +140,11 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
         ctx.profile(False)
         for layer, k in tab["kernel"].items():
             assert got.get(layer) == k, f"{layer}: table names {k}, plan ran {got.get(layer)}"
+    elif tuned == "table16gn":   # the many-tile producers really ran (else the fallback went untested)
+        got = planned_kernels(ctx)
+        ctx.profile(False)
+        for layer in ("downs.7.block1", "ups.5.block1", "downs.7.block2", "ups.5.block2"):
+            assert got.get(layer) == _TUNING16_GN[layer], (layer, got.get(layer))
     eps = eps.cpu().numpy()
     errs = [rms(eps[b], ref[b]) for b in range(B)]
     print(f"{dtype} {tuned} B={B} forward: row rms min {min(errs):.3e} max {max(errs):.3e} (ref rms {rms(ref, 0):.3f})")
