@@ -3,7 +3,9 @@
 // 256 workgroups x 8 waves, each wave issues NL DMAs of 1 KiB into its own LDS slab, then
 // s_waitcnt vmcnt(0).  Patterns: coalesced (lane l -> base + 16 l), stride320 (lane l -> base +
 // 320 l, a 160-channel bf16 pixel row per lane), block8 (8 lanes = 8 consecutive 16-B units of one
-// pixel row, 8 pixel rows per instruction).  L2-warm: every workgroup reads the same 512 KiB.
+// pixel row, 8 pixel rows per instruction), quad4 (4 lanes = 4 consecutive units of one pixel
+// row, 16 rows per instruction: the round-6 deep halo), unitmaj (16 lanes = one unit of 16 rows).
+// L2-warm: every workgroup reads the same 512 KiB.
 //   hipcc -O3 --offload-arch=gfx950 tools/mb_dma.hip -o tools/_mb_dma && ./tools/_mb_dma
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -22,7 +24,9 @@ __global__ __launch_bounds__(512) void k_dma(const char* __restrict__ src, unsig
     const char* p;
     if (PAT == 0) p = base + k * 1024 + lane * 16;
     else if (PAT == 1) p = base + (k % 20) * 16 + lane * 320 + (k / 20) * 64 * 320;
-    else p = base + (lane >> 3) * 320 + ((k % 2) * 8 + (lane & 7)) * 16 + (k / 2) * 8 * 320;
+    else if (PAT == 2) p = base + (lane >> 3) * 320 + ((k % 2) * 8 + (lane & 7)) * 16 + (k / 2) * 8 * 320;
+    else if (PAT == 3) p = base + (lane >> 2) * 320 + ((k % 5) * 4 + (lane & 3)) * 16 + (k / 5) * 16 * 320;
+    else p = base + (lane & 15) * 320 + ((k % 5) * 4 + (lane >> 4)) * 16 + (k / 5) * 16 * 320;
     __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)p,
                                      (__attribute__((address_space(3))) void*)(smem + wave * (NL * 1024) + k * 1024), 16, 0, 0);
   }
@@ -60,6 +64,8 @@ int main() {
   RUN(4, 0, "coalesced") RUN(8, 0, "coalesced") RUN(16, 0, "coalesced")
   RUN(4, 1, "stride320") RUN(8, 1, "stride320") RUN(16, 1, "stride320")
   RUN(4, 2, "block8") RUN(8, 2, "block8") RUN(16, 2, "block8")
+  RUN(4, 3, "quad4") RUN(8, 3, "quad4") RUN(16, 3, "quad4")
+  RUN(4, 4, "unitmaj") RUN(8, 4, "unitmaj") RUN(16, 4, "unitmaj")
   printf("MB_OK\n");
   return 0;
 }
