@@ -238,39 +238,6 @@ __host__ inline dim3 xcd_grid(int X, int Y, int Z) {
   return plain ? dim3(X, Y, Z) : dim3(X * Y * Z);
 }
 
-// L2 warm-up of the next conv's weight images (ConvArgs::pf_ptr / pf_bytes) while this conv runs:
-// the next layer's weights are otherwise first touched by all its blocks at once at its start, an
-// HBM round trip in every block's prologue (or, for the K-streamed tiles, in every chunk).  Each
-// block of the 1-D XCD-dealt grid (block id % 8 = its XCD, xcd_grid) touches its share of the
-// 128-byte lines, one lane per line, so every XCD's L2 ends up holding the whole image.  The loads
-// are 4-byte LDS-DMAs into a scratch slot nobody reads (256 B, block-private), issued by inline
-// asm: the compiler does not know them, so none of its waits is placed for them (its counted
-// waits stay correct: an unknown load only adds to the count, vmcnt is in order), and no VGPR is
-// held.  l2_warm_drain() (vmcnt(0)) must run before the scratch slot is reused or the block ends.
-// (NT = threads per block as a constant: blockDim would be read by a 16-bit vector load, whose
-// wait drains every load in flight)
-template <int NT, typename Args>   // ConvArgs (kernels.h)
-__device__ __forceinline__ void l2_warm(const Args& a, char* scratch) {
-  if (gridDim.y > 1 || gridDim.z > 1) return;            // plain (x, y, z) grid (SDDM_XCD=0 runs)
-  const int xcd = (int)blockIdx.x & 7, nbx = ((int)gridDim.x - xcd + 7) >> 3, r = (int)blockIdx.x >> 3;
-  const unsigned m0 = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(__attribute__((address_space(3))) char*)scratch);
-  const int wbase = __builtin_amdgcn_readfirstlane((int)threadIdx.x & ~63), lane = (int)threadIdx.x & 63;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const unsigned lines = (a.pf_bytes[k] + 127u) >> 7;
-    const unsigned lo = (unsigned)(((unsigned long long)r * lines) / (unsigned)nbx);
-    const unsigned hi = (unsigned)(((unsigned long long)(r + 1) * lines) / (unsigned)nbx);
-    for (unsigned l0 = lo + (unsigned)wbase; l0 < hi; l0 += NT) {   // wave-uniform
-      const unsigned l = min(l0 + (unsigned)lane, hi - 1);
-      const char* p = a.pf_ptr[k] + (size_t)l * 128;
-      unsigned save;                                     // m0 is the compiler's: restored in the same asm
-      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-                   : "=&s"(save) : "v"(p), "s"(m0) : "memory");
-    }
-  }
-}
-__device__ __forceinline__ void l2_warm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-
 // floor(n / d) for 0 <= n < 2^21 from the float reciprocal rd = 1 / d: ((n + .5) * rd) is off by
 // less than the .5 / d margin, so the truncation is exact (no integer division sequence).
 __device__ __forceinline__ int fdivi(int n, float rd) { return (int)(((float)n + 0.5f) * rd); }

@@ -83,9 +83,8 @@ __host__ __device__ inline DeepGeo deep_geo(bool s2, int TR, int TW, int MT) {
   return d;
 }
 
-// LDS byte layout of one block; region 0 (the staged image) is reused for the partial tiles; a
-// 256-byte L2 warm-up scratch slot (l2_warm) sits right after the image (live until the K loop ends)
-struct DeepLds { int gsc, total, pf; };
+// LDS byte layout of one block; region 0 (the staged image) is reused for the partial tiles
+struct DeepLds { int gsc, total; };
 
 template <typename T, int MT, int NW, int NB>
 __host__ __device__ inline DeepLds deep_layout(const DeepGeo& g, int Cin, int RC) {
@@ -94,8 +93,7 @@ __host__ __device__ inline DeepLds deep_layout(const DeepGeo& g, int Cin, int RC
   const int red = SLOTS * MT * NBP * 4;
   const int stage = (Cin / VE) * g.PLB + (RC / VE) * g.PLR;
   DeepLds L;
-  L.pf = stage;
-  L.gsc = stage + 256 > red ? stage + 256 : red;
+  L.gsc = stage > red ? stage : red;
   L.total = L.gsc + 2 * Cin * 4;
   return L;
 }
@@ -296,7 +294,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   if (gn) gl.finish(gf, b, gCA, gCB, gsc, gsc + Cin);
   dma_sync();                                            // every wave's DMAs landed, scale / shift visible
   DS_LANDED(a);
-  l2_warm<NT>(a, smem + lay.pf);                             // the next conv's weights, drained after the K loop
 
   // ---------------- 3. GroupNorm + SiLU in place (zero padding stays zero) ----------------
   if (gn) {
@@ -374,7 +371,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   DS_KLOOP(a);
 
   // ---------------- 5. reduce the partial tiles: red[slot][MT][NBP] ----------------
-  l2_warm_drain();                                  // the scratch slot is reused below
   lds_sync();                                       // every wave is done with the image
   float* red = (float*)smem;
   auto put = [&](int slot) {

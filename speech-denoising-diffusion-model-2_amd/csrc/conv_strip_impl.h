@@ -492,7 +492,6 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR_
       for (int fc = 0; fc < FC; ++fc) wreg[tap][fc] = load_planes<T>(abase + tap * 4 * UPL * WPL + fc * 256, WPL);
   }
   SDDM_STAMP(a, 3);
-  l2_warm<NT>(a, (char*)red);                                  // the next conv's weights (red is dead until the statistics)
   using yes = std::integral_constant<bool, true>;
   using no = std::integral_constant<bool, false>;
   for (int it = 0; it < iters - 2; it += 2) {            // period-2 rotation of the register sets
@@ -503,7 +502,6 @@ __global__ __launch_bounds__(MPI * 2) void conv_strip_kernel(ConvArgs a, int SR_
   body(no{}, no{}, iters - 1, rowsA, rowsB, r1B, r1A, r2B, r2A);
 
   SDDM_STAMP(a, 4);
-  l2_warm_drain();                                         // before red is written
   // ---- GroupNorm statistics of the strip: lanes -> waves -> block ----
   // every lane of a channel sums about the same shift badd, so the sums add directly: the 16
   // pixel lanes of a DPP row (VALU adds), then the waves through LDS

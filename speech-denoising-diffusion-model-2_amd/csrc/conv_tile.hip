@@ -300,7 +300,6 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     dma_sync();                                            // operand image 0, weights 0 (LDS-DMA)
   }
   SDDM_STAMP(a, 2);
-  l2_warm<NT>(a, (char*)(gsc + 2 * Cin));                      // the next conv's weights (drained after the K loop)
 #ifdef SDDM_STAMPS
   // timing ablations of the profiling build (SDDM_STAMPS_DBG): 4 no raw loads, 32 no weight DMA,
   // 8 no MFMAs, 2 no staging transform, 128 no output stores (results are garbage)
@@ -332,7 +331,6 @@ __global__ __launch_bounds__(64 * WPX * WCO) void conv_tile_kernel(ConvArgs a) {
     }
   }
   SDDM_STAMP(a, 4);
-  l2_warm_drain();
 
   // ---------------- epilogue ----------------
   T* out = (T*)a.out + (size_t)b * img_out * gCout;

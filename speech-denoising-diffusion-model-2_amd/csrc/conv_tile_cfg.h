@@ -118,10 +118,10 @@ __host__ __device__ inline TileGeo tile_geo(bool s2, int TR, int TW, int MT, boo
   return g;
 }
 
-// LDS: two operand images, two weight chunks (576 B per output channel), GroupNorm scale / shift,
-// the 256-byte L2 warm-up scratch slot (l2_warm); a single K chunk (nk == 1) needs one of each
+// LDS: two operand images, two weight chunks (576 B per output channel), GroupNorm scale / shift;
+// a single K chunk (nk == 1) needs one of each
 __host__ __device__ inline int tile_lds(const TileGeo& g, int NB, int Cin, int nbuf) {
-  return nbuf * g.ibb + nbuf * 576 * NB + 2 * Cin * 4 + 256;
+  return nbuf * g.ibb + nbuf * 576 * NB + 2 * Cin * 4;
 }
 
 __device__ __forceinline__ void glds16(const void* src, void* lds) {

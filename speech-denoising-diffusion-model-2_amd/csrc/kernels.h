@@ -83,10 +83,6 @@ struct ConvArgs {
   // 3x3 [Cout/16][Cin/32 * 9][64 lanes][8], res_conv [Cout/16][RC/32][64 lanes][8]
   const void* wgt_f;
   const void* res_wgt_f;
-  // L2 warm-up (l2_warm in conv_common.h): the weight images the NEXT conv of the step reads, in
-  // the format its kernel reads (null / 0: none)
-  const char* pf_ptr[2];
-  unsigned pf_bytes[2];
 };
 
 // ---- K-streamed implicit-GEMM tile convolution (conv_tile.hip, bf16 / f16 only) ----

@@ -852,26 +852,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
     return SDDM_OK;
   };
   sddm_ctx* ctx = c;
-  // L2 warm-up (l2_warm, conv_common.h): every conv launch touches the weight images of the next
-  // conv of the step, in the format that conv's kernel reads, so they are L2 hits when it starts.
-  // SDDM_L2_WARM=0 turns it off (A/B runs).
-  static const bool l2warm = !(std::getenv("SDDM_L2_WARM") && std::atoi(std::getenv("SDDM_L2_WARM")) == 0);
-  std::vector<std::pair<const char*, unsigned>> pf_main(prog.size(), {nullptr, 0u}), pf_res(prog.size(), {nullptr, 0u});
-  for (size_t i = 0; l2warm && i < prog.size(); ++i) {
-    if (prog[i].type != ST_CONV) continue;
-    ConvArgs x;
-    double by = 0, fl = 0;
-    if (const int r = conv_args(prog[i], x, by, fl)) return r;
-    const ConvChoice& ch = prog[i].ch;
-    const bool img_t = es == 2 && (ch.strip || ch.tile >= 0);   // chunk-major 16-bit image
-    const bool img_f = !ch.strip && ch.tile < 0;                // MFMA-fragment-major (conv_deep)
-    const void* w0 = img_f ? x.wgt_f : (img_t ? x.wgt_t : x.wgt);
-    const void* w1 = img_f ? x.res_wgt_f : (img_t ? x.res_wgt_t : x.res_wgt);
-    pf_main[i] = {(const char*)w0, (unsigned)((size_t)x.Cout * (x.CA + x.CB) * 9 * es)};
-    if (x.res_mode == 2) pf_res[i] = {(const char*)w1, (unsigned)((size_t)x.Cout * (x.RCA + x.RCB) * es)};
-  }
-  for (size_t si = 0; si < prog.size(); ++si) {
-    const Step& st = prog[si];
+  for (const Step& st : prog) {
     if (st.type == ST_CONVIN) {
       ConvInArgs a{};
       a.N = N; a.F = F; a.W = W; a.S = S; a.Cout = u.inner;
@@ -899,12 +880,6 @@ static int build_lane(sddm_ctx* c, Lane& L) {
       ConvArgs a;
       double bytes = 0, flops = 0;
       if (const int r = conv_args(st, a, bytes, flops)) return r;
-      for (size_t nj = si + 1; nj < prog.size(); ++nj)   // the next conv of the step
-        if (prog[nj].type == ST_CONV) {
-          a.pf_ptr[0] = pf_main[nj].first; a.pf_bytes[0] = pf_main[nj].second;
-          a.pf_ptr[1] = pf_res[nj].first; a.pf_bytes[1] = pf_res[nj].second;
-          break;
-        }
       const int Cin = a.CA + a.CB;
       const ConvChoice ch = st.ch;
       const bool s2 = st.s2 != 0;
