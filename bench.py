@@ -420,6 +420,7 @@ def main():
     ap.add_argument("--cpu-steps", type=int, default=3, help="CPU reverse steps at the config's batch (extrapolated x T)")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--no-variants", action="store_true", help="skip the same-run fp16 / fp32 sub-records")
+    ap.add_argument("--lane-rows", type=int, default=None, help="rows per UNet lane (default 16; 64 for B >= 64)")
     ap.add_argument("--f16-steps", type=int, default=5, help="timed runs of the 16-bit sub-record")
     ap.add_argument("--f32-steps", type=int, default=2, help="timed runs of the fp32 sub-record")
     ap.add_argument("--workload", default="unet", choices=["unet", "diffwave", "wavegrad"])
@@ -456,7 +457,7 @@ def main():
     network = config.init_obj("network", module_network, num_samples=N)
     model = config.init_obj("arch", module_arch, diffusion, network).to(dev).eval()
     model.compute_dtype = DTYPE_NAMES[args.dtype]
-    model.lane_rows = 64 if B >= 64 else None                     # 64-row lanes for large per-GPU batches
+    model.lane_rows = args.lane_rows or (64 if B >= 64 else None)  # 64-row lanes for large per-GPU batches
 
     cond_all = torch.from_numpy(noisy_speech(B * world, N, seed=1234)).to(dev)   # VoiceBank-DEMAND-shaped chunks
     result = {}

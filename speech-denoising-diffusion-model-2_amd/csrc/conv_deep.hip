@@ -104,38 +104,38 @@ template <int NW> struct DeepGN { static constexpr int GK = NW == 8 ? 4 : 8; };
 // deep kernel shapes (conv_tile_cfg.h ConvShape; cfg = pixels per tile): UNetModified2
 // config_unet.json at 16448 samples with the measured per-layer kernels of configs/conv_tuning.json
 static constexpr ConvShape kDeepShapes[] = {
-    {-1, 0, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},                  // generic (fields unused)
-    {32, 1, 2, 16, 32, 16, 96, 0, 96, 0, 0, 0, 0, 0, 4, 32},             // downs.6
-    {128, 0, 8, 16, 32, 16, 96, 0, 128, 0, 0, 0, 1, 0, 8, 32},           // downs.7.block1
-    {128, 0, 8, 16, 32, 16, 128, 0, 128, 96, 0, 2, 1, 0, 8, 32},         // downs.7.block2
-    {32, 1, 4, 8, 16, 8, 128, 0, 128, 0, 0, 0, 0, 0, 4, 32},             // downs.8
-    {64, 0, 8, 8, 16, 8, 128, 0, 160, 0, 0, 0, 1, 0, 4, 32},             // downs.9.block1
-    {64, 0, 8, 8, 16, 8, 160, 0, 160, 128, 0, 2, 1, 0, 4, 32},           // downs.9.block2
-    {32, 1, 8, 4, 8, 4, 160, 0, 160, 0, 0, 0, 0, 0, 4, 16},              // downs.10
-    {32, 0, 8, 4, 8, 4, 160, 0, 160, 0, 0, 0, 1, 0, 8, 16},              // mid.0.block1
-    {32, 0, 8, 4, 8, 4, 160, 0, 160, 0, 0, 1, 1, 0, 8, 16},              // mid.0.block2
-    {32, 0, 8, 4, 8, 4, 160, 160, 160, 0, 0, 0, 1, 0, 8, 16},            // ups.0.block1
-    {32, 0, 8, 4, 8, 4, 160, 0, 160, 160, 160, 2, 1, 0, 8, 16},          // ups.0.block2
-    {64, 0, 8, 8, 16, 8, 160, 0, 160, 0, 0, 0, 0, 1, 4, 32},             // ups.1
-    {32, 0, 4, 8, 16, 8, 160, 160, 128, 0, 0, 0, 1, 0, 8, 32},           // ups.2.block1
-    {32, 0, 4, 8, 16, 8, 128, 0, 128, 160, 160, 2, 1, 0, 4, 32},         // ups.2.block2
-    {32, 0, 4, 8, 16, 8, 128, 128, 128, 0, 0, 0, 1, 0, 8, 32},           // ups.3.block1
-    {32, 0, 4, 8, 16, 8, 128, 0, 128, 128, 128, 2, 1, 0, 4, 32},         // ups.3.block2
-    {128, 0, 8, 16, 32, 16, 128, 0, 128, 0, 0, 0, 0, 1, 4, 32},          // ups.4
-    {128, 0, 8, 16, 32, 16, 128, 128, 96, 0, 0, 0, 1, 0, 8, 32},         // ups.5.block1
-    {128, 0, 8, 16, 32, 16, 96, 0, 96, 128, 128, 2, 1, 0, 8, 32},        // ups.5.block2
-    {128, 0, 8, 16, 32, 16, 96, 96, 96, 0, 0, 0, 1, 0, 8, 32},           // ups.6.block1
-    {128, 0, 8, 16, 32, 16, 96, 0, 96, 96, 96, 2, 1, 0, 4, 32},          // ups.6.block2
-    // BASELINE config #5 per GPU (32832 samples, 64-row lanes, fp16) with its measured table
-    {64, 1, 4, 16, 64, 16, 96, 0, 96, 0, 0, 0, 0, 0, 4, 32, 1},          // c5:downs.6
-    {64, 0, 8, 8, 32, 8, 128, 0, 160, 0, 0, 0, 1, 0, 4, 32, 1},          // c5:downs.9.block1
-    {64, 0, 8, 8, 32, 8, 160, 0, 160, 128, 0, 2, 1, 0, 4, 32, 1},        // c5:downs.9.block2
-    {32, 1, 8, 4, 16, 4, 160, 0, 160, 0, 0, 0, 0, 0, 4, 32, 1},          // c5:downs.10
-    {32, 0, 8, 4, 16, 4, 160, 0, 160, 0, 0, 0, 1, 0, 4, 32, 1},          // c5:mid.0.block1
-    {32, 0, 8, 4, 16, 4, 160, 0, 160, 0, 0, 1, 1, 0, 4, 32, 1},          // c5:mid.0.block2
-    {32, 0, 8, 4, 16, 4, 160, 160, 160, 0, 0, 0, 1, 0, 4, 32, 1},        // c5:ups.0.block1
-    {32, 0, 8, 4, 16, 4, 160, 0, 160, 160, 160, 2, 1, 0, 4, 32, 1},      // c5:ups.0.block2
-    {64, 0, 8, 8, 32, 8, 160, 0, 160, 0, 0, 0, 0, 1, 4, 32, 1},          // c5:ups.1
+    {-1, 0, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0},   // generic (fields unused)
+    // generated by tools/gen_shapes.py from configs/conv_tuning.json (do not edit by hand)
+    {32, 1, 2, 16, 32, 16, 96, 0, 96, 0, 0, 0, 0, 0, 4, 32, 0},  // downs.6
+    {128, 0, 8, 16, 32, 16, 96, 0, 128, 0, 0, 0, 1, 0, 8, 32, 0},  // downs.7.block1
+    {128, 0, 8, 16, 32, 16, 128, 0, 128, 96, 0, 2, 1, 0, 8, 32, 0},  // downs.7.block2
+    {32, 1, 4, 8, 16, 8, 128, 0, 128, 0, 0, 0, 0, 0, 4, 32, 0},  // downs.8
+    {64, 0, 8, 8, 16, 8, 128, 0, 160, 0, 0, 0, 1, 0, 4, 32, 0},  // downs.9.block1
+    {64, 0, 8, 8, 16, 8, 160, 0, 160, 128, 0, 2, 1, 0, 4, 32, 0},  // downs.9.block2
+    {32, 1, 8, 4, 8, 4, 160, 0, 160, 0, 0, 0, 0, 0, 4, 16, 0},  // downs.10
+    {32, 0, 8, 4, 8, 4, 160, 0, 160, 0, 0, 0, 1, 0, 8, 16, 0},  // mid.0.block1
+    {32, 0, 8, 4, 8, 4, 160, 0, 160, 0, 0, 1, 1, 0, 8, 16, 0},  // mid.0.block2
+    {32, 0, 8, 4, 8, 4, 160, 160, 160, 0, 0, 0, 1, 0, 8, 16, 0},  // ups.0.block1
+    {32, 0, 8, 4, 8, 4, 160, 0, 160, 160, 160, 2, 1, 0, 8, 16, 0},  // ups.0.block2
+    {64, 0, 8, 8, 16, 8, 160, 0, 160, 0, 0, 0, 0, 1, 4, 32, 0},  // ups.1
+    {32, 0, 4, 8, 16, 8, 160, 160, 128, 0, 0, 0, 1, 0, 8, 32, 0},  // ups.2.block1
+    {32, 0, 4, 8, 16, 8, 128, 0, 128, 160, 160, 2, 1, 0, 4, 32, 0},  // ups.2.block2
+    {32, 0, 4, 8, 16, 8, 128, 128, 128, 0, 0, 0, 1, 0, 8, 32, 0},  // ups.3.block1
+    {32, 0, 4, 8, 16, 8, 128, 0, 128, 128, 128, 2, 1, 0, 4, 32, 0},  // ups.3.block2
+    {128, 0, 8, 16, 32, 16, 128, 0, 128, 0, 0, 0, 0, 1, 4, 32, 0},  // ups.4
+    {128, 0, 8, 16, 32, 16, 128, 128, 96, 0, 0, 0, 1, 0, 8, 32, 0},  // ups.5.block1
+    {128, 0, 8, 16, 32, 16, 96, 0, 96, 128, 128, 2, 1, 0, 8, 32, 0},  // ups.5.block2
+    {128, 0, 8, 16, 32, 16, 96, 96, 96, 0, 0, 0, 1, 0, 8, 32, 0},  // ups.6.block1
+    {128, 0, 8, 16, 32, 16, 96, 0, 96, 96, 96, 2, 1, 0, 4, 32, 0},  // ups.6.block2
+    {64, 1, 4, 16, 64, 16, 96, 0, 96, 0, 0, 0, 0, 0, 4, 32, 1},  // c5:downs.6
+    {64, 0, 8, 8, 32, 8, 128, 0, 160, 0, 0, 0, 1, 0, 4, 32, 1},  // c5:downs.9.block1
+    {64, 0, 8, 8, 32, 8, 160, 0, 160, 128, 0, 2, 1, 0, 4, 32, 1},  // c5:downs.9.block2
+    {32, 1, 8, 4, 16, 4, 160, 0, 160, 0, 0, 0, 0, 0, 4, 32, 1},  // c5:downs.10
+    {32, 0, 8, 4, 16, 4, 160, 0, 160, 0, 0, 0, 1, 0, 4, 32, 1},  // c5:mid.0.block1
+    {32, 0, 8, 4, 16, 4, 160, 0, 160, 0, 0, 1, 1, 0, 4, 32, 1},  // c5:mid.0.block2
+    {32, 0, 8, 4, 16, 4, 160, 160, 160, 0, 0, 0, 1, 0, 4, 32, 1},  // c5:ups.0.block1
+    {32, 0, 8, 4, 16, 4, 160, 0, 160, 160, 160, 2, 1, 0, 4, 32, 1},  // c5:ups.0.block2
+    {64, 0, 8, 8, 32, 8, 160, 0, 160, 0, 0, 0, 0, 1, 4, 32, 1},  // c5:ups.1
 };
 static constexpr int kNDeepShapes = (int)(sizeof(kDeepShapes) / sizeof(kDeepShapes[0]));
 

@@ -93,7 +93,7 @@ def run(config, model, loader, dataset, device, logger=None, seed=None):
     return log
 
 
-def main(config, seed=None):
+def main(config, seed=None, lane_rows=None):
     logger = config.get_logger("infer")
     if "infer_data_loader" not in config.config:
         config.config["infer_data_loader"] = {"type": "InferDataLoader", "args": {"batch_size": 4, "num_workers": 2}}
@@ -111,6 +111,12 @@ def main(config, seed=None):
     device = torch.device("cuda", torch.cuda.current_device())
     _, _, model = module_arch.build_from_config(config, module_diffusion, module_network, module_arch, device)
     model = model.to(device).eval()
+    # rows per lane of the UNet plan (library default 16): small batches (a few chunks of
+    # InferDataLoader's 4 files) run faster on lane_rows 4 / 8 plans, which have their own measured
+    # kernel tables in configs/conv_tuning.json.  --lane-rows or a top-level "lane_rows" config key.
+    lane_rows = lane_rows or config.config.get("lane_rows")
+    if lane_rows:
+        model.lane_rows = int(lane_rows)
     if config.resume is not None:
         logger.info("Loading checkpoint: {} ...".format(config.resume))
         model.load_state_dict(state_dict_from_checkpoint(str(config.resume)))
@@ -123,9 +129,14 @@ if __name__ == "__main__":
     args.add_argument("-r", "--resume", default=None, type=str, help="checkpoint path")
     args.add_argument("-d", "--device", default=None, type=str, help="indices of GPUs to enable")
     args.add_argument("--seed", default=None, type=int, help="noise seed (default: torch's generator)")
-    seed = None
+    args.add_argument("--lane-rows", default=None, type=int, help="rows per UNet lane (default: the library's 16)")
+    seed, lane = None, None
     if "--seed" in sys.argv:
         k = sys.argv.index("--seed")
         seed = int(sys.argv[k + 1])
         del sys.argv[k:k + 2]
-    main(ConfigParser.from_args(args), seed)
+    if "--lane-rows" in sys.argv:
+        k = sys.argv.index("--lane-rows")
+        lane = int(sys.argv[k + 1])
+        del sys.argv[k:k + 2]
+    main(ConfigParser.from_args(args), seed, lane)

@@ -277,6 +277,39 @@ def repo_tuning_table(N, lane_batch):
     return text, (tabs[0] if tabs else None)
 
 
+@pytest.mark.parametrize("lane", [4, 8])
+def test_unet_forward_small_lane_measured_table(torch_cuda, lane):
+    """infer.py's batches (InferDataLoader batch_size 4: a few chunks per batch, reference
+    infer.py:70-77) on lane_rows = 4 / 8 plans: the plan takes the repository's table measured for
+    that lane batch (tools/gpu_tile_sweep.sh at --lane-rows 4 / 8), runs its kernel on every layer,
+    and matches the oracle on distinct rows at distinct noise levels."""
+    N = 16448
+    cond, x_t, nl, ref = bench_rows(N, 16)
+    cond, x_t, nl, ref = cond[:lane], x_t[:lane], nl[:lane], ref[:lane]
+    text, tab = repo_tuning_table(N, lane)
+    assert tab is not None, f"no measured table for lane batch {lane}"
+    dev = torch_cuda.device("cuda", 0)
+    cfg = unet_config(N, ("linear", 100, 1e-6, 1e-3))
+    cfg["lane_rows"] = lane
+    ctx = sddm_hip.Context(cfg, 0, "bfloat16")
+    for k, v in unet_params(N).items():
+        ctx.load_param("noise_estimate_model." + k, v)
+    ctx.set_conv_tuning(text)
+    ctx.profile(True)
+    eps = torch_cuda.full((lane, 1, N), float("nan"), device=dev)
+    ctx.network_forward(torch_cuda.from_numpy(cond).to(dev), torch_cuda.from_numpy(x_t).to(dev),
+                        torch_cuda.from_numpy(nl).to(dev), eps)
+    torch_cuda.cuda.synchronize()
+    got = planned_kernels(ctx)
+    ctx.profile(False)
+    for layer, k in tab["kernel"].items():
+        assert got.get(layer) == k, f"{layer}: table names {k}, plan ran {got.get(layer)}"
+    eps = eps.cpu().numpy()
+    errs = [rms(eps[b], ref[b]) for b in range(lane)]
+    print(f"lane_rows {lane} measured table: row rms max {max(errs):.3e}")
+    assert np.isfinite(eps).all() and max(errs) <= 2.5e-2
+
+
 _CONFIG5_ROWS = {}
 
 

@@ -96,3 +96,18 @@ def test_row_invariants():
                 assert r["TR"] == r["nb"] and r["TW"] == r["Wo"], f"{name}: strip rows encode TR = strip rows, TW = W"
             if kind == "deep":
                 assert r["TR"] * r["TW"] <= r["cfg"] and r["nw"] in (4, 8) and r["nb"] in (16, 32), name
+
+
+def test_rows_are_the_generators_output():
+    """The three tables are generated from configs/conv_tuning.json by tools/gen_shapes.py (the
+    runtime's layer walk and tile rules for the kernel each measured table names): the committed
+    rows are exactly its output, every field, so a re-measured table is applied by re-running it."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    import gen_shapes
+    gen = gen_shapes.generate()
+    for kind, rows in _tables().items():
+        assert [(n, r) for n, r in rows[1:]] == [(n, dict(r)) for n, r in gen[kind]], kind
+    for kind, (path, table) in gen_shapes.TABLES.items():
+        text = open(os.path.join(CSRC, path)).read()
+        assert gen_shapes.splice(text, table, gen_shapes.render(gen[kind])) == text, path
