@@ -156,7 +156,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
   constexpr int TPP = NB / 4;          // epilogue threads per pixel (4 channels each)
   constexpr int PPI = NT / TPP;        // pixels per epilogue pass
   constexpr int EIT = (MT + PPI - 1) / PPI;
-  static_assert(NB == 16 || NB == 32, "16 or 32 output channels per block");
+  static_assert(NB == 16 || NB == 32 || NB == 64, "16, 32 or 64 output channels per block");
   constexpr int SLOTS = (NW == 8 && MT >= 128) ? 4 : NW;
 
   int tile, b, zb;
@@ -429,7 +429,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void conv_deep_kernel(ConvArgs a) 
     // thread per channel in wave order
     auto wred = [](float x) {
       if constexpr (TPP == 4) x += dpp_f32<0x124>(x);   // row_ror:4
-      x += dpp_f32<0x128>(x);                          // row_ror:8
+      if constexpr (TPP <= 8) x += dpp_f32<0x128>(x);   // row_ror:8
       x += __shfl_xor(x, 16);
       return x + __shfl_xor(x, 32);
     };
@@ -491,7 +491,14 @@ static hipError_t deep_go(const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
     hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT, NW, DV, NB, SH>), grid, blk, lay.total, s, a); \
     return hipGetLastError();                                                                 \
   }
-  if constexpr (SH > 0) {                                 // one ring depth per specialised shape
+  if constexpr (NB == 64) {                               // 4 fragments per K step: a 4-step ring
+    if constexpr (sizeof(T) == 4) {
+      return hipErrorInvalidValue;                        // (16-bit only)
+    } else {
+      hipLaunchKernelGGL((conv_deep_kernel<T, S2, MT, NW, 4, NB, SH>), grid, blk, lay.total, s, a);
+      return hipGetLastError();
+    }
+  } else if constexpr (SH > 0) {                          // one ring depth per specialised shape
     constexpr ConvShape c = kDeepShapes[SH];
     constexpr int spw = (((c.CA + c.CB) / 32) * 9 + (c.res == 2 ? (c.RCA + c.RCB) / 32 : 0) + NW - 1) / NW;
     constexpr int DS = (NW == 4 || MT >= 128 || spw <= 8) ? 8 : 12;
@@ -524,7 +531,8 @@ static bool deep_shape_go(int mt, int nw, int nb, bool s2, const ConvArgs& a, in
   }
 }
 
-// nb: output channels per block (32, or 16 for twice the blocks with half the weight bytes each)
+// nb: output channels per block (32; 16 for twice the blocks with half the weight bytes each; 64
+// for half the blocks, each transforming its input halo once for twice the output channels)
 template <typename T>
 static hipError_t deep_dispatch(int mt, int nw, int nb, bool s2, const ConvArgs& a, int B, hipStream_t s, size_t* lo) {
   static const bool generic = std::getenv("SDDM_NO_DEEP_SHAPES") != nullptr;   // A/B runs
@@ -539,6 +547,9 @@ static hipError_t deep_dispatch(int mt, int nw, int nb, bool s2, const ConvArgs&
   SDDM_DEEP(false, 16, 4, 16) SDDM_DEEP(false, 32, 4, 16) SDDM_DEEP(false, 64, 4, 16) SDDM_DEEP(false, 128, 4, 16)
   SDDM_DEEP(true, 16, 4, 16) SDDM_DEEP(true, 32, 4, 16) SDDM_DEEP(true, 64, 4, 16)
   SDDM_DEEP(false, 32, 8, 16) SDDM_DEEP(false, 64, 8, 16) SDDM_DEEP(false, 128, 8, 16)
+  // 64-channel blocks (16-bit): a tile's halo transformed by half as many channel blocks (round 6)
+  SDDM_DEEP(false, 32, 4, 64) SDDM_DEEP(false, 64, 4, 64) SDDM_DEEP(false, 32, 8, 64)
+  SDDM_DEEP(true, 32, 4, 64) SDDM_DEEP(true, 64, 4, 64)
 #undef SDDM_DEEP
   if (lo) *lo = (size_t)1 << 40;
   return hipErrorInvalidValue;
@@ -551,9 +562,9 @@ hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B
   return deep_dispatch<f16_t>(mt, nw, nb, s2, a, B, s, nullptr);
 }
 
-int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps) {
+int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps, int nb) {
   const int spw = (ksteps + nw - 1) / nw;
-  if (dtype == DT_F32) return 4;
+  if (dtype == DT_F32 || nb == 64) return 4;
   if (nw == 4 || mt >= 128) return 8;
   return deep_ring<bf16_t, 64, 8>(spw);
 }

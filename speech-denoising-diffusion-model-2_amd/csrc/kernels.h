@@ -97,7 +97,7 @@ size_t conv_tile_lds_bytes(int cfg, bool s2, const ConvArgs& a);
 // mt: output pixels per block (32 / 64 / 128); s2: stride-2 Downsample
 hipError_t launch_conv_deep(int dtype, int mt, bool s2, const ConvArgs& a, int B, hipStream_t s);
 size_t conv_deep_lds_bytes(int dtype, int mt, bool s2, const ConvArgs& a);
-int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps);   // the D template argument (profiles)
+int conv_deep_ring_depth(int dtype, int mt, int nw, int ksteps, int nb);   // the D template argument (profiles)
 
 // LDS per workgroup every launcher and planner sizes against: gfx950's 160 KiB (sddm_create fails
 // on a device that offers less, so no plan is built for LDS the device does not have)

@@ -517,7 +517,8 @@ static bool choose_deep(int dt, int B, ConvArgs a, bool s2, ConvChoice& ch, int 
   // 16-channel blocks only where asked for (tuning table or SDDM_DEEP_CFG): twice the blocks, each
   // with half the weight bytes (the per-CU load volume bounds these layers) but the input halo
   // transformed twice as often
-  const int nb = want_mt ? (want_nb ? want_nb : 32) : (force_nb ? force_nb : 32);
+  // (a forced block width that does not divide a layer's channels leaves that layer at 32)
+  const int nb = want_mt ? (want_nb ? want_nb : 32) : (force_nb && a.Cout % force_nb == 0 ? force_nb : 32);
   if (a.Cout % nb) return false;
   const int nz = a.Cout / nb;
   a.deep_nb = nb;
@@ -939,7 +940,7 @@ static int build_lane(sddm_ctx* c, Lane& L) {
           snprintf(ki, sizeof(ki), "%s", kn);
         else
           snprintf(ki, sizeof(ki), "conv_deep_kernel<%s,%d,%d,%d,%d,%d>", dt_name(dt), s2 ? 1 : 0, ch.mt, ch.nw,
-                   conv_deep_ring_depth(dt, ch.mt, ch.nw, (Cin / 32) * 9 + (a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0)),
+                   conv_deep_ring_depth(dt, ch.mt, ch.nw, (Cin / 32) * 9 + (a.res_mode == 2 ? (a.RCA + a.RCB) / 32 : 0), ch.nb),
                    ch.nb);
         L.ops.back().kinst = ki;
       }

@@ -99,6 +99,12 @@ _TUNING16 = {"downs.7.block1": "deep:64:8:16", "downs.7.block2": "deep:128:4:16"
              "ups.0.block2": "deep:16:4:16", "ups.1": "deep:64:4:16", "ups.4": "deep:128:8:16",
              "ups.5.block1": "deep:64:8:16", "ups.6.block2": "deep:128:4:16"}
 
+# conv_deep with 64-channel blocks (the Cout = 128 layers): 4 and 8 waves, 32- and 64-pixel tiles,
+# stride 2, upsample, virtual concat, identity residual and res_conv chunks
+_TUNING64 = {"downs.7.block1": "deep:32:4:64", "downs.7.block2": "deep:64:4:64", "downs.8": "deep:32:4:64",
+             "ups.2.block1": "deep:32:8:64", "ups.2.block2": "deep:64:4:64", "ups.3.block1": "deep:64:4:64",
+             "ups.3.block2": "deep:32:4:64", "ups.4": "deep:64:4:64"}
+
 # producers of 32 tiles per image at 32x16 (16-pixel deep tiles): their consumers (downs.7.block2,
 # ups.5.block2) combine 128 / 96 (tile, channel) statistics per group, more than one GroupNorm load
 # round trip holds (64), so they take the fp64 two-pass finalize (gn_fused_prologue)
@@ -109,7 +115,8 @@ _TUNING16_GN = {**_TUNING16, "downs.7.block1": "deep:16:4:16", "ups.5.block1": "
 @pytest.mark.parametrize("dtype,tol,tuned", [("float32", 1e-4, None), ("bfloat16", 2.5e-2, None),
                                             ("bfloat16", 2.5e-2, "table"), ("bfloat16", 2.5e-2, "repo"),
                                             ("bfloat16", 2.5e-2, "table16"), ("float32", 1e-4, "table16"),
-                                            ("bfloat16", 2.5e-2, "table16gn"), ("float16", 5e-3, None)])
+                                            ("bfloat16", 2.5e-2, "table16gn"), ("bfloat16", 2.5e-2, "table64"),
+                                            ("float16", 5e-3, "table64"), ("float16", 5e-3, None)])
 def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     """B=16 x N=16448 (the bench shape), 16 distinct rows at 16 noise levels: the kernels and tiles
     picked for a full lane (and per-layer kernels set through sddm_set_conv_tuning: a table
@@ -120,10 +127,11 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     cond, x_t, nl, ref = bench_rows(N, B)
     dev = torch_cuda.device("cuda", 0)
     ctx = make_ctx(N, dtype)
-    if tuned in ("table", "table16", "table16gn"):
+    if tuned in ("table", "table16", "table16gn", "table64"):
         # per-layer kernels everywhere
         ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N,
-                             "kernel": {"table": _TUNING, "table16": _TUNING16, "table16gn": _TUNING16_GN}[tuned]})
+                             "kernel": {"table": _TUNING, "table16": _TUNING16, "table16gn": _TUNING16_GN,
+                                        "table64": _TUNING64}[tuned]})
         ctx.profile(True)
     elif tuned == "repo":
         text, tab = repo_tuning_table(N, B)
@@ -145,6 +153,11 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
         ctx.profile(False)
         for layer in ("downs.7.block1", "ups.5.block1", "downs.7.block2", "ups.5.block2"):
             assert got.get(layer) == _TUNING16_GN[layer], (layer, got.get(layer))
+    elif tuned == "table64":     # every forced 64-channel layer ran its kernel
+        got = planned_kernels(ctx)
+        ctx.profile(False)
+        for layer, k in _TUNING64.items():
+            assert got.get(layer) == k, (layer, got.get(layer))
     eps = eps.cpu().numpy()
     errs = [rms(eps[b], ref[b]) for b in range(B)]
     print(f"{dtype} {tuned} B={B} forward: row rms min {min(errs):.3e} max {max(errs):.3e} (ref rms {rms(ref, 0):.3f})")

@@ -95,7 +95,7 @@ def test_row_invariants():
             if kind == "strip":
                 assert r["TR"] == r["nb"] and r["TW"] == r["Wo"], f"{name}: strip rows encode TR = strip rows, TW = W"
             if kind == "deep":
-                assert r["TR"] * r["TW"] <= r["cfg"] and r["nw"] in (4, 8) and r["nb"] in (16, 32), name
+                assert r["TR"] * r["TW"] <= r["cfg"] and r["nw"] in (4, 8) and r["nb"] in (16, 32, 64), name
 
 
 def test_rows_are_the_generators_output():

@@ -14,11 +14,11 @@ SDDM_NO_TILE=1 timeout -k 10 120 python tools/profile_ops.py --timesteps 10 $SWE
 head -2 $SD/deep.log | tail -1
 timeout -k 10 120 python tools/profile_ops.py --timesteps 10 $SWEEP_OPS_ARGS --json $SD/auto.json > $SD/auto.log 2>&1 || { echo FAIL_auto; tail -5 $SD/auto.log; exit 1; }
 head -2 $SD/auto.log | tail -1
-for c in 0 1 2 3 4 5 6 7 8 9 10 11 12; do
+for c in ${SWEEP_TILE_CFGS:-0 1 2 3 4 5 6 7 8 9 10 11 12}; do
 SDDM_TILE_CFG=$c timeout -k 10 120 python tools/profile_ops.py --timesteps 10 $SWEEP_OPS_ARGS --json $SD/t$c.json > $SD/t$c.log 2>&1 || { echo FAIL_$c; tail -5 $SD/t$c.log; exit 1; }
 echo "cfg $c: $(head -2 $SD/t$c.log | tail -1)"
 done
-for dc in 16:4:16 32:4:16 32:8:16 64:4:16 64:8:16 128:8:16 128:4:16 32:8:32 64:8:32 128:8:32 64:4:32 128:4:32 32:4:32; do
+for dc in ${SWEEP_DEEP_CFGS:-16:4:16 32:4:16 32:8:16 64:4:16 64:8:16 128:8:16 128:4:16 32:8:32 64:8:32 128:8:32 64:4:32 128:4:32 32:4:32 32:4:64 64:4:64 32:8:64}; do
 n=$(echo $dc | tr ':' '_')
 SDDM_NO_TILE=1 SDDM_DEEP_CFG=$dc timeout -k 10 120 python tools/profile_ops.py --timesteps 10 $SWEEP_OPS_ARGS --json $SD/d$n.json > $SD/d$n.log 2>&1 || { echo FAIL_d$n; tail -5 $SD/d$n.log; exit 1; }
 echo "deep $dc: $(head -2 $SD/d$n.log | tail -1)"
