@@ -147,6 +147,22 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
   if (a.t_dev && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *a.t_dev -= 1;
   SDDM_STAMP_AT(a, 0, blockIdx.x + blockIdx.y * (a.F / a.TR));
   const int S = a.S, F = a.F, W = a.W, IW = W + 2, IH = a.TR + 2;
+  // bias and weights first: issued before the frame image loads, so their round trip overlaps
+  // the image's instead of following it (stamps: the staging phase was two round trips, 4.5 us)
+  constexpr int KPL = sizeof(T) == 4 ? 5 : 8;   // K values per lane per pixel fragment
+  float bias[2][4];
+#pragma unroll
+  for (int fc = 0; fc < 2; ++fc)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[fc][i] = a.bias[fc * 16 + 4 * g + i];
+  float wf[2][KPL];                             // weights as MFMA A operands (rows = output channels)
+#pragma unroll
+  for (int j = 0; j < KPL; ++j) {
+    const int k = sizeof(T) == 4 ? 4 * j + g : 8 * g + j;
+    const int kk = k < 18 ? k : 0;              // (clamped: unconditional loads, masked below)
+#pragma unroll
+    for (int fc = 0; fc < 2; ++fc) wf[fc][j] = a.w[(fc * 16 + (lane & 15)) * 18 + kk];
+  }
   {  // every load of the frame image issued before the first is stored (clamped addresses:
      // a load under a condition is waited for at the branch join)
     const float* c0 = a.cond + (size_t)b * a.N;
@@ -170,16 +186,9 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
       if (i < IH * IW) { img[0][i] = cv[k]; img[1][i] = xv[k]; }
     }
   }
-  float bias[2][4];
-#pragma unroll
-  for (int fc = 0; fc < 2; ++fc)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) bias[fc][i] = a.bias[fc * 16 + 4 * g + i];
   // this lane's K entries k -> (signal, dy, dx) as offsets into the frame image (k >= 18: zero)
-  constexpr int KPL = sizeof(T) == 4 ? 5 : 8;   // K values per lane per pixel fragment
   int koff[KPL];
   bool kok[KPL];
-  float wf[2][KPL];                             // weights as MFMA A operands (rows = output channels)
 #pragma unroll
   for (int j = 0; j < KPL; ++j) {
     const int k = sizeof(T) == 4 ? 4 * j + g : 8 * g + j;
@@ -187,7 +196,7 @@ __global__ __launch_bounds__(256) void conv_in_kernel(ConvInArgs a) {
     const int kk = kok[j] ? k : 0, ch = kk >= 9 ? 1 : 0, tap = kk - 9 * ch;
     koff[j] = ch * IMAX + (tap / 3) * IW + (tap % 3);
 #pragma unroll
-    for (int fc = 0; fc < 2; ++fc) wf[fc][j] = kok[j] ? a.w[(fc * 16 + (lane & 15)) * 18 + k] : 0.f;
+    for (int fc = 0; fc < 2; ++fc) wf[fc][j] = kok[j] ? wf[fc][j] : 0.f;
   }
   f16x8 wh[2], wl[2];
 #pragma unroll
@@ -447,6 +456,10 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
     }
   };
   load_pass(wave);
+  // the conv weights of this lane's 8 channels, before the GroupNorm wait (one round trip, not two)
+  float wraw[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) wraw[j] = a.w[(8 * g + j) * 9 + (tapr < 9 ? tapr : 0)];
   gl.finish(gf, b, C, 0, gs, gs + C);
   lds_sync();                                        // scale / shift visible (loads stay in flight)
   SDDM_STAMP_AT(a, 1, ftile + b * (F / FT));
@@ -457,7 +470,7 @@ __global__ __launch_bounds__(NT) void final_kernel(FinalArgs a) {
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int c = 8 * g + j;
-    wv[j] = tapr < 9 ? a.w[c * 9 + tapr] * -kLN2 : 0.f;
+    wv[j] = tapr < 9 ? wraw[j] * -kLN2 : 0.f;
     sc[j] = gs[c] * -kL2E;
     sh[j] = gs[C + c] * -kL2E;
   }
