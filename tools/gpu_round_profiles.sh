@@ -16,7 +16,7 @@ OPS_ARGS="--dtype f16" TRAFFIC_KEY="16448 16 f16" TRAFFIC_OUT=profiles/${R}_f16_
 cp profiles/${R}_f16_hbm_traffic.json $O/
 timeout -k 10 900 python3 bench.py > $O/${R}_bench.json.log 2>&1 || { echo BENCH_FAIL; tail -5 $O/${R}_bench.json.log; exit 1; }
 tail -1 $O/${R}_bench.json.log | cut -c1-200
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_bench -o run -- python3 bench.py --timesteps 100 --steps 1 --warmup 1 --no-cpu-baseline > $O/${R}_bench_T100_rocprof.json.log 2>&1 || { echo PROF_FAIL; exit 1; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_bench -o run -- python3 bench.py --timesteps 100 --steps 1 --warmup 1 --no-cpu-baseline --no-variants > $O/${R}_bench_T100_rocprof.json.log 2>&1 || { echo PROF_FAIL; exit 1; }
 cp gpurun_out/prof_bench/run_kernel_stats.csv $O/${R}_kernel_stats_T100_B16_bf16.csv
 # (the fp16 twin and fp32 are the headline line's same-run `variants` since round 6)
 if [ -n "$CONFIG5" ]; then   # config #5 per GPU: PMC traffic, then the bench line that reads it
