@@ -393,6 +393,188 @@ __global__ __launch_bounds__(256, (PREW || sizeof(T) == 4) ? 2 : 3) void dw_laye
   }
 }
 
+// ---------------- ping-pong residual layer (16-bit) ----------------
+// The same layer as dw_layer_kernel, with the staging and the GEMMs of a CU split between two wave
+// groups that work on different tiles: a persistent block of 8 waves walks a strided list of
+// 128-sample tiles; waves 4-7 (staging group) load tile k+1 -- y = x + diffusion projection over the
+// dilated window, the raw residual rows -- into one of two LDS slots while waves 0-3 (GEMM group) run
+// tile k's dilated-conv GEMM, gated activation, output_residual GEMM and epilogue from the other.
+// Two workgroup barriers per tile: the GEMM group's z hand-off (z goes to its own LDS buffer) and
+// the slot swap.  The staging group's global loads are in flight during the GEMM group's MFMAs, so
+// a CU waits on memory only when a tile's loads outlast its GEMMs.
+constexpr int DW_PP_Y = 3 * 8 * DW_MS * 16;                  // yin: 3 taps x 8 planes x 128 samples (16-bit)
+constexpr int DW_PP_SLOT = DW_PP_Y + DW_MS * (DW_C * 2 + 16);  // + raw residual rows
+constexpr int DW_PP_LDS = 2 * DW_PP_SLOT + 8 * DW_MS * 16;     // two slots + z [8 planes][128][16 B]
+
+template <typename T, int GW>
+__global__ __launch_bounds__(64 * (GW + 4), 1) void dw_layer_pp_kernel(DWLayerArgs a) {
+  static_assert(sizeof(T) == 2 && (GW == 4 || GW == 8), "16-bit, 4 or 8 GEMM waves");
+  constexpr int FPW = 8 * 4 / GW;                  // 16-sample fragments per GEMM wave
+  constexpr int ES = 2, VE = 8, UPS = 8, PB = 8;  // 16-byte units per sample; samples per 64-unit group
+  constexpr int PLANE = DW_MS * 16, XS = DW_C * ES + 16, MAXU = 12;
+  typedef T vec4 __attribute__((ext_vector_type(4)));
+  typedef T vec __attribute__((ext_vector_type(VE)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* zl = smem + 2 * DW_PP_SLOT;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int N = a.N, d = a.dil, G = gridDim.x;
+  const int tpc = (N + DW_MS - 1) / DW_MS, ntiles = tpc * a.B;
+  const int t_now = a.t_dev ? *a.t_dev : 0;
+  const bool win = d <= 64;
+  const int ROWS = win ? (DW_MS + 2 * d + PB - 1) / PB * PB : DW_MS, TAPS = win ? 1 : 3;
+  const int PL = win ? (ROWS * 16 + 255) / 256 * 256 : PLANE;
+  const int NUr = TAPS * ROWS * UPS;               // <= MAXU * 256 (checked by the launcher)
+  int tile = blockIdx.x;
+
+  if (wave >= GW) {
+    // ---------------- staging group ----------------
+    const int st = tid - 64 * GW;                      // 0 .. 255
+    const int qs = (st & 63) / PB;                 // channel unit of every unit this thread stages
+    f32x4 reg[MAXU];
+    float dsv[VE];
+    auto issue = [&](int tl) {                     // global loads of tile tl into registers
+      const int b = tl / tpc, n0 = (tl - b * tpc) * DW_MS;
+      const T* xin = (const T*)a.x_in + (size_t)b * N * DW_C;
+      const float* ds = a.ds + ((size_t)(a.ds_per_b ? b : t_now) * a.L + a.layer) * DW_C;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) dsv[e] = ds[qs * VE + e];
+#pragma unroll
+      for (int k = 0; k < MAXU; ++k) {
+        const int u = min(st + k * 256, NUr - 1);
+        const int tap = u / (ROWS * UPS), r = u - tap * (ROWS * UPS);
+        const int grp = r >> 6, j = r & 63, q = j / PB, s = grp * PB + (j % PB);
+        const int n = win ? n0 - d + s : n0 + s + (tap - 1) * d;
+        reg[k] = *(const f32x4*)(xin + (size_t)min(max(n, 0), N - 1) * DW_C + q * VE);
+      }
+    };
+    auto land = [&](int tl, char* slot) {          // transform + LDS stores (same unit map as issue)
+      const int b = tl / tpc, n0 = (tl - b * tpc) * DW_MS;
+      (void)b;
+      char* yin = slot;
+      char* xl = slot + DW_PP_Y;
+#pragma unroll
+      for (int k = 0; k < MAXU; ++k) {
+        const int u = st + k * 256;
+        if (u < NUr) {
+          const int tap = u / (ROWS * UPS), r = u - tap * (ROWS * UPS);
+          const int grp = r >> 6, j = r & 63, q = j / PB, s = grp * PB + (j % PB);
+          const int n = win ? n0 - d + s : n0 + s + (tap - 1) * d;
+          const bool ok = n >= 0 && n < N;
+          const int c = n - n0;                    // the centre rows also go to the residual image, raw
+          if ((win || tap == 1) && c >= 0 && c < DW_MS) *(f32x4*)(xl + c * XS + q * 16) = reg[k];
+          vec v = __builtin_bit_cast(vec, reg[k]);
+#pragma unroll
+          for (int e = 0; e < VE; ++e) v[e] = from_f32<T>(ok ? to_f32<T>(v[e]) + dsv[e] : 0.f);
+          *(f32x4*)(yin + (tap * UPS + q) * PL + s * 16) = __builtin_bit_cast(f32x4, v);
+        }
+      }
+    };
+    // (a second register set, issuing tile k+2 while tile k+1 lands, measured no faster: 193.4 vs
+    // 190.5 us per layer at config #3)
+    if (tile < ntiles) { issue(tile); land(tile, smem); }
+    lds_sync();
+    for (int k = 0; tile < ntiles; ++k, tile += G) {
+      const int next = tile + G;
+      if (next < ntiles) issue(next);
+      lds_sync();                                  // (the GEMM group's z hand-off; the loads stay in flight)
+      if (next < ntiles) land(next, smem + ((k + 1) & 1) * DW_PP_SLOT);
+      lds_sync();                                  // slot swap
+    }
+    return;
+  }
+
+  // ---------------- GEMM group: wave = channel quarter wq x sample part (FPW fragments from p0) ----------------
+  const int wq = wave & 3, p0 = (wave >> 2) * FPW;
+  const int cg = wq * 16 + 4 * g;                // gate rows cg..cg+3; filter rows cg + 64
+  const T* w1 = (const T*)a.w1;
+  const T* w2 = (const T*)a.w2;
+  Frag<T> aw1[6][2], aw2[2];
+#pragma unroll
+  for (int s = 0; s < 6; ++s)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      aw1[s][c] = load_frag<T>((const char*)(w1 + (size_t)(c * 64 + wq * 16 + (lane & 15)) * 192 + s * 32 + g * 8));
+#pragma unroll
+  for (int s = 0; s < 2; ++s) aw2[s] = load_frag<T>((const char*)(w2 + (size_t)(wq * 16 + (lane & 15)) * DW_C + s * 32 + g * 8));
+  float bg[4], bfl[4], br[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { bg[i] = a.b1[cg + i]; bfl[i] = a.b1[cg + 64 + i]; br[i] = a.b2[cg + i]; }
+  const float ir2 = 0.707106769084930419921875f;   // (float)(1 / sqrt(2.0)), as dw_layer_kernel's 16-bit path
+  // conditioner rows of this wave's channels: loaded one tile ahead (issued after the gate of the
+  // previous tile, so they are in flight during its output_residual GEMM, epilogue and barriers)
+  vec4 cnd[2][FPW];
+  const T* cb = (const T*)a.cond + (size_t)a.layer * a.B * N * 128;   // layer-major: one stream per layer
+  auto load_cond = [&](int tl) {
+    const int b = tl / tpc, n0 = (tl - b * tpc) * DW_MS;
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) {
+      const int n = min(n0 + (p0 + p) * 16 + (lane & 15), N - 1);
+      const T* cp = cb + ((size_t)b * N + n) * 128;
+      cnd[0][p] = *(const vec4*)(cp + cg);
+      cnd[1][p] = *(const vec4*)(cp + cg + 64);
+    }
+  };
+  if (tile < ntiles) load_cond(tile);
+  lds_sync();                                      // tile 0 staged
+  for (int k = 0; tile < ntiles; ++k, tile += G) {
+    const int b = tile / tpc, n0 = (tile - b * tpc) * DW_MS;
+    const char* yin = smem + (k & 1) * DW_PP_SLOT;
+    const char* xl = yin + DW_PP_Y;
+    f32x4 acc[2][FPW];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int p = 0; p < FPW; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+      const int tap = s >> 1, half = s & 1;
+      const char* pb = yin + ((win ? 0 : tap * UPS) + (half * 32 + g * 8) / VE) * PL + ((win ? tap * d : 0) + (lane & 15)) * 16;
+#pragma unroll
+      for (int p = 0; p < FPW; ++p) {
+        const Frag<T> bf = load_planes<T>(pb + (p0 + p) * 256, PL);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], aw1[s][c], bf);
+      }
+    }
+    const bool full = n0 + DW_MS <= N;
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) {
+      float z[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float gate = acc[0][p][i] + bg[i] + to_f32<T>(cnd[0][p][i]);
+        const float filt = acc[1][p][i] + bfl[i] + to_f32<T>(cnd[1][p][i]);
+        z[i] = dw_sigmoid_fast(gate) * dw_tanh_fast(filt);
+      }
+      store4<T>((T*)(zl + (cg / VE) * PLANE + ((p0 + p) * 16 + (lane & 15)) * 16 + (cg % VE) * ES), z[0], z[1], z[2], z[3]);
+      const int n = n0 + (p0 + p) * 16 + (lane & 15);
+      if (full || n < N) store4<T>((T*)a.z + (((size_t)a.layer * a.B + b) * N + n) * DW_C + cg, z[0], z[1], z[2], z[3]);
+    }
+    if (tile + G < ntiles) load_cond(tile + G);
+    lds_sync();                                    // z hand-off (the z stores and next conditioner loads stay in flight)
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) acc[0][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const char* pb = zl + ((s * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
+#pragma unroll
+      for (int p = 0; p < FPW; ++p) mfma_frag(acc[0][p], aw2[s], load_planes<T>(pb + (p0 + p) * 256, PLANE));
+    }
+    T* xo = (T*)a.x_out + (size_t)b * N * DW_C;
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) {
+      const int n = n0 + (p0 + p) * 16 + (lane & 15);
+      if (!full && n >= N) continue;
+      const vec4 xv = *(const vec4*)(xl + ((p0 + p) * 16 + (lane & 15)) * XS + cg * ES);
+      store4<T>(xo + (size_t)n * DW_C + cg, (to_f32<T>(xv[0]) + (acc[0][p][0] + br[0])) * ir2,
+                (to_f32<T>(xv[1]) + (acc[0][p][1] + br[1])) * ir2, (to_f32<T>(xv[2]) + (acc[0][p][2] + br[2])) * ir2,
+                (to_f32<T>(xv[3]) + (acc[0][p][3] + br[3])) * ir2);
+    }
+    lds_sync();                                    // slot swap
+  }
+}
+
 size_t dw_layer_lds_bytes(int dtype) {
   const int es = dtype == DT_F32 ? 4 : 2, ups = DW_C * es / 16;
   return (size_t)3 * ups * DW_MS * 16 + (size_t)DW_MS * (DW_C * es + 16);   // staging + residual rows
@@ -405,6 +587,22 @@ hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
     const bool win = a.dil <= 64;
     const int rows = win ? (DW_MS + 2 * a.dil + pb - 1) / pb * pb : DW_MS;
     if (dtype != DT_F32 && (win ? 1 : 3) * rows * ups > 12 * 256) return hipErrorInvalidValue;
+  }
+  // 16-bit: the ping-pong kernel (config #3: 215.5 -> 190.5 us per layer); SDDM_DW_NOPP=1 runs the
+  // one-phase kernel (A/B knob)
+  static const bool nopp = std::getenv("SDDM_DW_NOPP") != nullptr;
+  if (!nopp && dtype != DT_F32) {
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0)
+        return hipErrorInvalidValue;
+    }
+    const int ntiles = (int)grid.x * (int)grid.y;
+    const dim3 pgrid(ntiles < ncu ? ntiles : ncu);
+    if (dtype == DT_BF16) hipLaunchKernelGGL((dw_layer_pp_kernel<bf16_t, 4>), pgrid, dim3(512), DW_PP_LDS, s, a);
+    else hipLaunchKernelGGL((dw_layer_pp_kernel<f16_t, 4>), pgrid, dim3(512), DW_PP_LDS, s, a);
+    return hipGetLastError();
   }
   const size_t lds = dw_layer_lds_bytes(dtype);
   static const bool nopre = std::getenv("SDDM_DW_NOPRE") != nullptr;   // experiment knob

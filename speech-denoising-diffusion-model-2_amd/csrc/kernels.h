@@ -85,6 +85,21 @@ struct ConvArgs {
   const void* res_wgt_f;
 };
 
+// ---- the UNet's bottom level in one launch (conv_chain.hip, bf16 / f16): downs.<last> (stride-2),
+// mid.0 (ResnetBlock, identity residual), ups.0 (ResnetBlock over cat(mid, downs.<last>), res_conv)
+struct ChainArgs {
+  const void* x;              // [B][2H][2W][C] the level's input (downs.<last-1> output)
+  void* out;                  // [B][H][W][C] ups.0.block2 output
+  const void* wgt[5];         // MFMA-fragment-major 3x3 images (ConvArgs::wgt_f layout) of the five convs
+  const void* res_wgt;        // ups.0 res_conv, [C/16][2C/32][64 lanes][8]
+  const float* bias[5];       // (ups.0.block2's includes the res_conv bias)
+  const float* gamma[4]; const float* beta[4];   // GroupNorm of mid.0.block1/2, ups.0.block1 (2C), ups.0.block2
+  const float* temb[2];       // noise-embedding projection of mid.0 / ups.0 (row stride temb_ld)
+  int temb_ld; const int* t_dev; int temb_per_b;
+  int C, H, W, groups; float eps;
+};
+hipError_t launch_conv_chain(int dtype, const ChainArgs& a, int B, hipStream_t s);
+
 // ---- K-streamed implicit-GEMM tile convolution (conv_tile.hip, bf16 / f16 only) ----
 // cfg: tile configuration index (kTileCfgs in conv_tile.hip); s2: stride-2 Downsample
 struct TileCfg { int wpx, wco, fp, fc; };   // waves along pixels / channels, 16-wide fragments per wave

@@ -500,6 +500,7 @@ struct ConvChoice {
   int mt = 0, ckb = 0, nw = 4, nb = 32;           // conv_deep: pixels per block, input chunks, waves, channels
   int tile = -1;                                  // conv_tile configuration (16-bit dtypes), -1: none
   int TR = 0, TW = 0, tiles_x = 0, n_tiles = 0;  // stats tiling of the output
+  int chain = 0;                                  // 1: part of the bottom-level chain launch (conv_chain.hip)
 };
 
 // conv_deep tile (pixels per block) and waves per block.  A block's time is dominated by its
@@ -726,7 +727,13 @@ static int build_lane(sddm_ctx* c, Lane& L) {
         if (kind == 3) { wm = kt->second.a; wn = kt->second.b; wb = kt->second.c; }
       }
     }
-    return choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka, wb);
+    // "chain": the layer runs inside the bottom-level chain launch; its tensor keeps the tiling the
+    // heuristic would give it (only the chain reads or writes it)
+    const bool chain = kind == 4 && dt != DT_F32;
+    if (kind == 4) kind = 0;
+    const bool ok = choose_conv(dt, PB, Cin, RC, res_mode, Ho, Wo, cout, s2, up, ch, wm, wn, kind, ka, wb);
+    ch.chain = chain ? 1 : 0;
+    return ok;
   };
   const int TRin = 512 / W;
   if (u.inner != 32 || 512 % W || F % TRin || (TRin + 1) * S + W + 2 > 1024)
@@ -853,7 +860,56 @@ static int build_lane(sddm_ctx* c, Lane& L) {
     return SDDM_OK;
   };
   sddm_ctx* ctx = c;
-  for (const Step& st : prog) {
+  for (size_t si = 0; si < prog.size(); ++si) {
+    const Step& st = prog[si];
+    if (st.type == ST_CONV && st.ch.chain) {
+      // the bottom level in one launch (conv_chain.hip): the last Downsample and the four convs of
+      // mid.0 and ups.0, every one marked "chain" in the tuning table
+      if (si + 4 >= prog.size()) FAIL(SDDM_ERR_SHAPE, "chain: %s is not followed by mid.0 / ups.0", st.w.c_str());
+      const Step* S5[5] = {&prog[si], &prog[si + 1], &prog[si + 2], &prog[si + 3], &prog[si + 4]};
+      const char* want[5] = {nullptr, "mid.0.block1", "mid.0.block2", "ups.0.block1", "ups.0.block2"};
+      for (int k = 0; k < 5; ++k)
+        if (S5[k]->type != ST_CONV || !S5[k]->ch.chain || (k > 0 && S5[k]->w != want[k]) || (k == 0 && !S5[k]->s2))
+          FAIL(SDDM_ERR_SHAPE, "chain: the tuning table must mark the last Downsample, mid.0.block1/2 and ups.0.block1/2 (got %s)",
+               S5[k]->w.c_str());
+      ConvArgs ca[5];
+      double bytes = 0, flops = 0;
+      for (int k = 0; k < 5; ++k) {
+        double by = 0, fl = 0;
+        if (const int r = conv_args(*S5[k], ca[k], by, fl)) return r;
+        flops += fl;
+      }
+      const int Cc = ca[0].Cout, Hc = ca[0].Ho, Wc = ca[0].Wo;
+      if (ca[1].CA != Cc || ca[3].CA != Cc || ca[3].CB != Cc || ca[4].res_mode != 2 || ca[4].RCA != Cc || ca[4].RCB != Cc ||
+          ca[2].res_mode != 1 || ca[3].srcB != ca[0].out || ca[4].rawB != ca[0].out)
+        FAIL(SDDM_ERR_SHAPE, "chain: unexpected bottom-level wiring");
+      ChainArgs x{};
+      x.x = ca[0].srcA; x.out = ca[4].out;
+      for (int k = 0; k < 5; ++k) { x.wgt[k] = ca[k].wgt_f; x.bias[k] = ca[k].bias; }
+      for (int k = 0; k < 4; ++k) { x.gamma[k] = ca[k + 1].gamma; x.beta[k] = ca[k + 1].beta; }
+      x.res_wgt = ca[4].res_wgt_f;
+      x.temb_ld = c->SC; x.C = Cc; x.H = Hc; x.W = Wc; x.groups = u.groups; x.eps = 1e-5f;
+      bytes = (double)B * (2 * Hc) * (2 * Wc) * Cc * es + (double)B * Hc * Wc * Cc * es;
+      for (int k = 0; k < 5; ++k) bytes += (double)ca[k].Cout * (ca[k].CA + ca[k].CB) * 9 * es;
+      bytes += (double)Cc * 2 * Cc * es;
+      const int toff_m = c->temb_off.at("mid.0"), toff_u = c->temb_off.at("ups.0");
+      std::string nm;
+      for (int k = 0; k < 5; ++k) nm += (k ? "+" : "") + S5[k]->w;
+      L.ops.push_back({2, bytes, flops, [lp, x, dt, B, toff_m, toff_u](hipStream_t s) {
+                          ChainArgs y = x;
+                          y.temb[0] = lp->rs.temb ? lp->rs.temb + toff_m : nullptr;
+                          y.temb[1] = lp->rs.temb ? lp->rs.temb + toff_u : nullptr;
+                          y.temb_per_b = lp->rs.temb_per_b;
+                          y.t_dev = lp->rs.t_dev;
+                          return launch_conv_chain(dt, y, B, s);
+                        }, nm + "[chain]"});
+      char kn[96];
+      snprintf(kn, sizeof(kn), "conv_chain_kernel<%s,%d,%d,%d>", dt_name(dt), Cc, Hc, Wc);
+      L.ops.back().kname = kn;
+      L.ops.back().kinst = kn;
+      si += 4;
+      continue;
+    }
     if (st.type == ST_CONVIN) {
       ConvInArgs a{};
       a.N = N; a.F = F; a.W = W; a.S = S; a.Cout = u.inner;
@@ -1615,7 +1671,7 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
         if (kv.second.kind != Json::ARR || kv.second.arr.size() != 2) FAIL(SDDM_ERR_INVALID_ARG, "deep.%s: [mt, nw]", kv.first.c_str());
         tt.deep_tune[kv.first] = {(int)kv.second.arr[0].num, (int)kv.second.arr[1].num};
       }
-    // "kernel": {"<layer>": "strip" | "tile:<cfg>" | "deep" | "deep:<mt>:<nw>[:<nb>]"}
+    // "kernel": {"<layer>": "strip" | "tile:<cfg>" | "deep" | "deep:<mt>:<nw>[:<nb>]" | "chain"}
     if (t.has("kernel"))
       for (const auto& kv : t.at("kernel").obj) {
         if (kv.second.kind != Json::STR) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: a string", kv.first.c_str());
@@ -1625,6 +1681,7 @@ int sddm_set_conv_tuning(sddm_ctx* c, const char* json) {
         else if (v.rfind("tile:", 0) == 0) { k.kind = 2; k.a = std::atoi(v.c_str() + 5); }
         else if (v == "deep") k.kind = 3;
         else if (v.rfind("deep:", 0) == 0) { k.kind = 3; std::sscanf(v.c_str() + 5, "%d:%d:%d", &k.a, &k.b, &k.c); }
+        else if (v == "chain") k.kind = 4;
         else FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: unknown choice '%s'", kv.first.c_str(), v.c_str());
         if (k.kind == 2 && (k.a < 0 || k.a >= conv_tile_ncfg())) FAIL(SDDM_ERR_INVALID_ARG, "kernel.%s: tile configuration %d", kv.first.c_str(), k.a);
         tt.kern_tune[kv.first] = k;

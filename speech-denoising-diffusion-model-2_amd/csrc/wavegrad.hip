@@ -227,9 +227,12 @@ constexpr int WGL_MC = 128, WGL_HALO = 8;
 // TW = waves along time: block = 2 x TW waves = 128 channels x 64 TW positions (TW = 4 halves the
 // per-position weight traffic from L2 on the long levels).  The 3-tap variants without FiLM are
 // held to 168 registers (three waves per SIMD, three blocks per CU: 135 vs 148 and 103 vs 114 us
-// per launch); the FiLM variant spills there (364 vs 252 us) and the 1-tap ones gain nothing
-template <typename T, int PRE, int KT, int TW>
-__global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2) void wg_conv_lds_kernel(WGConvArgs a) {
+// per launch); the FiLM variant spills there (364 vs 252 us) and the 1-tap ones gain nothing.
+// WD: the weight image of each chunk goes global -> LDS by DMA (global_load_lds, no staging
+// registers), single-buffered: issued after the barrier that frees the image, waited before the
+// chunk's MFMAs; with WD the FiLM variant is held to three blocks per CU
+template <typename T, int PRE, int KT, int TW, int WD = 0>
+__global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && (PRE != 2 || WD)) ? 3 : 2) void wg_conv_lds_kernel(WGConvArgs a) {
 #pragma clang fp contract(off)
   constexpr int NT = 128 * TW, WGL_MT = 64 * TW;
   constexpr int ES = (int)sizeof(T), UE = 16 / ES;         // elements per 16-byte unit
@@ -237,7 +240,8 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
   constexpr int RS = UPR * 16 + 16;                         // padded LDS row stride (bytes)
   constexpr int SROWS = WGL_MT + 2 * WGL_HALO;
   constexpr int NBU = SROWS * UPR, NAU = KT * WGL_MC * UPR;
-  constexpr int PB = (NBU + NT - 1) / NT, PA = (NAU + NT - 1) / NT;
+  constexpr int PB = (NBU + NT - 1) / NT, PA = WD ? 1 : (NAU + NT - 1) / NT;
+  static_assert(!WD || (ES == 2 && (KT * WGL_MC) % 64 == 0), "weight DMA: 16-bit, whole 64-slot runs");
   // 16-bit storage: plane-major images (a plane = one 16-byte channel unit of every row, plane
   // stride 0 mod 256 B) with the row slot XOR-swizzled by 2 x plane, so the staging stores (8-lane
   // groups: 2 rows x 4 planes) and the MFMA operand reads (ds_read_b128 lane groups mixing 8 rows
@@ -278,11 +282,29 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
         screg[j % PF] = *(const f32x4*)(fp + Cin);
       }
     }
+    if (!WD) {
 #pragma unroll
-    for (int j = 0; j < PA; ++j) {
-      const int u = tid + j * NT;
-      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
-      if (u < NAU) areg[j] = *(const f32x4*)(W + ((size_t)(cob + co) * KT + k) * Cin + c0 + q * UE);
+      for (int j = 0; j < PA; ++j) {
+        const int u = tid + j * NT;
+        const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
+        if (u < NAU) areg[j] = *(const f32x4*)(W + ((size_t)(cob + co) * KT + k) * Cin + c0 + q * UE);
+      }
+    }
+  };
+  // weight image of chunk c0 by DMA: plane q holds KT * 128 slots in 64-slot runs, one run per wave
+  // instruction; lane l of a run starting at slot s0 fetches row r = (s0 + l) ^ 2q (the swizzle)
+  auto wdma = [&](int c0) {
+    constexpr int RUNS = UPR * KT * WGL_MC / 64, RPW = (RUNS + NT / 64 - 1) / (NT / 64);
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int run = wave * RPW + i;                  // wave-uniform
+      if (run < RUNS) {
+        const int q = run / (KT * WGL_MC / 64), s0 = (run - q * (KT * WGL_MC / 64)) * 64;
+        const int r = (s0 + lane) ^ (q << 1), k = r / WGL_MC, co = r - k * WGL_MC;
+        __builtin_amdgcn_global_load_lds(
+            (const __attribute__((address_space(1))) void*)(W + ((size_t)(cob + co) * KT + k) * Cin + c0 + q * UE),
+            (__attribute__((address_space(3))) void*)(wl + q * PSW + s0 * 16), 16, 0, 0);
+      }
     }
   };
   auto lstore = [&]() {
@@ -309,12 +331,14 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
       }
       *(f32x4*)(slab + sadr(r, q)) = v;
     }
+    if (!WD) {
 #pragma unroll
-    for (int j = 0; j < PA; ++j) {
-      const int u = tid + j * NT;
-      if (u >= NAU) continue;
-      const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
-      *(f32x4*)(wl + wadr(k * WGL_MC + co, q)) = areg[j];
+      for (int j = 0; j < PA; ++j) {
+        const int u = tid + j * NT;
+        if (u >= NAU) continue;
+        const int k = u / (WGL_MC * UPR), rem = u - k * (WGL_MC * UPR), co = rem / UPR, q = rem - co * UPR;
+        *(f32x4*)(wl + wadr(k * WGL_MC + co, q)) = areg[j];
+      }
     }
   };
 
@@ -329,8 +353,10 @@ __global__ __launch_bounds__(128 * TW, (TW == 2 && KT == 3 && PRE != 2) ? 3 : 2)
   gload(0);
   for (int cc = 0; cc < ncs; ++cc) {
     __syncthreads();
+    if (WD) wdma(cc * 32);
     lstore();
-    __syncthreads();
+    if (WD) dma_sync();                                  // the weight DMAs landed, the slab stored
+    else __syncthreads();
     if (cc + 1 < ncs) gload((cc + 1) * 32);
 #pragma unroll
     for (int k = 0; k < KT; ++k) {
@@ -425,7 +451,10 @@ bool wg_conv_uses_lds(const WGConvArgs& a) {
 template <typename T, int PRE, int TW>
 static void wg_conv_lds_dispatch(const WGConvArgs& a, hipStream_t s) {
   const dim3 grid((a.Tc + 64 * TW - 1) / (64 * TW), a.Cout / WGL_MC, a.B);
+  static const bool wd = std::getenv("SDDM_WG_FILM_DMA") != nullptr;   // experiment knob
   if (a.K == 1) hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE == 2 ? 0 : PRE, 1, TW>), grid, dim3(128 * TW), 0, s, a);
+  else if (PRE == 2 && TW == 2 && sizeof(T) == 2 && wd)
+    hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3, TW, sizeof(T) == 2 ? 1 : 0>), grid, dim3(128 * TW), 0, s, a);
   else hipLaunchKernelGGL((wg_conv_lds_kernel<T, PRE, 3, TW>), grid, dim3(128 * TW), 0, s, a);
 }
 

@@ -25,7 +25,7 @@ if VARIANT:
 else:
     BUILD = os.path.join(HERE, "_build")
     LIB = os.path.join(HERE, "libsddm_hip.so")
-SOURCES = ["kernels.hip", "conv_strip.hip", "conv_strip_bf16.hip", "conv_strip_f16.hip", "conv_strip_f32.hip", "conv_deep.hip", "conv_tile.hip", "diffwave.hip", "wavegrad.hip", "q_sample.hip", "stft.hip", "sddm_runtime.cpp",
+SOURCES = ["kernels.hip", "conv_strip.hip", "conv_strip_bf16.hip", "conv_strip_f16.hip", "conv_strip_f32.hip", "conv_deep.hip", "conv_tile.hip", "conv_chain.hip", "diffwave.hip", "wavegrad.hip", "q_sample.hip", "stft.hip", "sddm_runtime.cpp",
            "schedule.cpp"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = os.environ.get("SDDM_OFFLOAD_ARCH", "gfx950")

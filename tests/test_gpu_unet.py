@@ -105,6 +105,10 @@ _TUNING64 = {"downs.7.block1": "deep:32:4:64", "downs.7.block2": "deep:64:4:64",
              "ups.2.block1": "deep:32:8:64", "ups.2.block2": "deep:64:4:64", "ups.3.block1": "deep:64:4:64",
              "ups.3.block2": "deep:32:4:64", "ups.4": "deep:64:4:64"}
 
+# the bottom level (downs.10, mid.0, ups.0) as one launch (conv_chain.hip)
+_CHAIN = {"downs.10": "chain", "mid.0.block1": "chain", "mid.0.block2": "chain", "ups.0.block1": "chain",
+          "ups.0.block2": "chain"}
+
 # producers of 32 tiles per image at 32x16 (16-pixel deep tiles): their consumers (downs.7.block2,
 # ups.5.block2) combine 128 / 96 (tile, channel) statistics per group, more than one GroupNorm load
 # round trip holds (64), so they take the fp64 two-pass finalize (gn_fused_prologue)
@@ -116,7 +120,8 @@ _TUNING16_GN = {**_TUNING16, "downs.7.block1": "deep:16:4:16", "ups.5.block1": "
                                             ("bfloat16", 2.5e-2, "table"), ("bfloat16", 2.5e-2, "repo"),
                                             ("bfloat16", 2.5e-2, "table16"), ("float32", 1e-4, "table16"),
                                             ("bfloat16", 2.5e-2, "table16gn"), ("bfloat16", 2.5e-2, "table64"),
-                                            ("float16", 5e-3, "table64"), ("float16", 5e-3, None)])
+                                            ("float16", 5e-3, "table64"), ("bfloat16", 2.5e-2, "chain"),
+                                            ("float16", 5e-3, "chain"), ("float16", 5e-3, None)])
 def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     """B=16 x N=16448 (the bench shape), 16 distinct rows at 16 noise levels: the kernels and tiles
     picked for a full lane (and per-layer kernels set through sddm_set_conv_tuning: a table
@@ -127,11 +132,11 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
     cond, x_t, nl, ref = bench_rows(N, B)
     dev = torch_cuda.device("cuda", 0)
     ctx = make_ctx(N, dtype)
-    if tuned in ("table", "table16", "table16gn", "table64"):
+    if tuned in ("table", "table16", "table16gn", "table64", "chain"):
         # per-layer kernels everywhere
         ctx.set_conv_tuning({"lane_batch": B, "dtype": dtype, "num_samples": N,
                              "kernel": {"table": _TUNING, "table16": _TUNING16, "table16gn": _TUNING16_GN,
-                                        "table64": _TUNING64}[tuned]})
+                                        "table64": _TUNING64, "chain": _CHAIN}[tuned]})
         ctx.profile(True)
     elif tuned == "repo":
         text, tab = repo_tuning_table(N, B)
@@ -153,10 +158,10 @@ def test_unet_forward_bench_batch(torch_cuda, dtype, tol, tuned):
         ctx.profile(False)
         for layer in ("downs.7.block1", "ups.5.block1", "downs.7.block2", "ups.5.block2"):
             assert got.get(layer) == _TUNING16_GN[layer], (layer, got.get(layer))
-    elif tuned == "table64":     # every forced 64-channel layer ran its kernel
+    elif tuned in ("table64", "chain"):     # every forced layer ran its kernel
         got = planned_kernels(ctx)
         ctx.profile(False)
-        for layer, k in _TUNING64.items():
+        for layer, k in {"table64": _TUNING64, "chain": _CHAIN}[tuned].items():
             assert got.get(layer) == k, (layer, got.get(layer))
     eps = eps.cpu().numpy()
     errs = [rms(eps[b], ref[b]) for b in range(B)]
@@ -272,6 +277,10 @@ def planned_kernels(ctx):
         name, _, tag = o["name"].partition("[")
         if tag:
             tag = tag.rstrip("]")
+            if tag == "chain":               # one launch for the bottom level's five convs
+                for layer in name.split("+"):
+                    got[layer] = "chain"
+                continue
             got[name] = "strip" if tag == "strip" else (
                 "tile:" + tag[4:] if tag.startswith("tile") else "deep:" + tag[4:].replace("_", ":"))
     return got
