@@ -106,23 +106,34 @@ __global__ __launch_bounds__(256) void dw_upsample1_kernel(DWUpArgs a) {
   }
 }
 
-// second pass, written sample-major [B][N][Kp] in T (zero rows h >= H pad K to a multiple of 32)
+// second pass, written sample-major [B][N][Kp] in T (zero rows h >= H pad K to a multiple of 32):
+// one thread per output sample n, all Kp values of it as 16-byte vectors; neighbouring lanes read
+// the same or adjacent first-pass columns (coalesced)
 template <typename T>
 __global__ __launch_bounds__(256) void dw_upsample2_kernel(DWUpArgs a) {
+  constexpr int VE = 16 / (int)sizeof(T);
+  typedef T vec __attribute__((ext_vector_type(VE)));
   const int Wm = 16 * a.F, N = 256 * a.F;
-  const int64_t total = (int64_t)a.B * N * a.Kp;
-  T* out = (T*)a.out;
+  const int64_t total = (int64_t)a.B * N;
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
-    const int h = (int)(i % a.Kp);
-    const int64_t bn = i / a.Kp;
-    const int n = (int)(bn % N), b = (int)(bn / N);
-    const float v = h < a.H ? dw_up_point(a.mid + (size_t)b * a.H * Wm, a.H, Wm, a.k2, a.b2[0], h, n) : 0.f;
-    out[i] = from_f32<T>(v);
+    const int n = (int)(i % N), b = (int)(i / N);
+    const float* mid = a.mid + (size_t)b * a.H * Wm;
+    T* out = (T*)a.out + i * a.Kp;
+    for (int h0 = 0; h0 < a.Kp; h0 += VE) {
+      vec v;
+#pragma unroll
+      for (int j = 0; j < VE; ++j) {
+        const int h = h0 + j;
+        v[j] = from_f32<T>(h < a.H ? dw_up_point(mid, a.H, Wm, a.k2, a.b2[0], h, n) : 0.f);
+      }
+      *(vec*)(out + h0) = v;
+    }
   }
 }
 
 hipError_t launch_dw_upsample(int dtype, const DWUpArgs& a, hipStream_t s) {
-  const int64_t t1 = (int64_t)a.B * a.H * 16 * a.F, t2 = (int64_t)a.B * 256 * a.F * a.Kp;
+  if (a.Kp % 8) return hipErrorInvalidValue;
+  const int64_t t1 = (int64_t)a.B * a.H * 16 * a.F, t2 = (int64_t)a.B * 256 * a.F;
   hipLaunchKernelGGL(dw_upsample1_kernel, dim3((unsigned)std::min<int64_t>((t1 + 255) / 256, 65535)), dim3(256), 0, s, a);
   const dim3 g2((unsigned)std::min<int64_t>((t2 + 255) / 256, 65535));
   if (dtype == DT_F32) hipLaunchKernelGGL(dw_upsample2_kernel<float>, g2, dim3(256), 0, s, a);
@@ -132,11 +143,19 @@ hipError_t launch_dw_upsample(int dtype, const DWUpArgs& a, hipStream_t s) {
 }
 
 // ---------------- conditioner projections of all layers (step-invariant GEMM) ----------------
-// cond[l][b][n][co] = sum_k Wc[l][co][k] spec[b][n][k] + bc[l][co]; block = 128 samples x 128 co
+// cond[l][b][n][co] = sum_k Wc[l][co][k] spec[b][n][k] + bc[l][co]; block = 128 samples x 128 co.
+// Block order: the L layer blocks of one sample tile are consecutive on one XCD (blocks i and i + 8
+// share an XCD under round-robin dealing), so the tile's spectrogram rows (Kp up to 544 channels:
+// 139 KB in 16 bits) come from HBM once and from that XCD's L2 for the other layers (tile-major
+// over all layers at once re-read the whole 1.1 GB spectrogram per layer: 18 GB fetched, 17 ms)
 template <typename T>
 __global__ __launch_bounds__(256) void dw_cond_kernel(DWCondArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
-  const int n0 = blockIdx.x * DW_MS, b = blockIdx.y, l = blockIdx.z;
+  const int tpc = (a.N + DW_MS - 1) / DW_MS, ntl = tpc * a.B;
+  const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+  const int tile = xcd + 8 * (j / a.L), l = j - (j / a.L) * a.L;
+  if (tile >= ntl) return;                          // block-uniform (padding of the last group of 8)
+  const int b = tile / tpc, n0 = (tile - b * tpc) * DW_MS;
   const T* W = (const T*)a.w + (size_t)l * 128 * a.Kp;
   const T* S = (const T*)a.spec + (size_t)b * a.N * a.Kp;
   f32x4 acc[2][8];
@@ -162,25 +181,52 @@ __global__ __launch_bounds__(256) void dw_cond_kernel(DWCondArgs a) {
       for (int p = 0; p < 8; ++p) mfma_frag(acc[c][p], af[c], bf[p]);
   }
   T* out = (T*)a.out;
+  if constexpr (sizeof(T) == 2) {
+    // the block's 128 x 128 tile goes through LDS so that HBM sees whole 256-byte rows (a contiguous
+    // 32 KB run: out is [L][B][N][128]); 8-byte accumulator stores scatter 32-byte pieces
+    constexpr int RS = 128 * 2 + 16;                 // padded row stride (bytes)
+    __shared__ __attribute__((aligned(16))) char tl[DW_MS * RS];
 #pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const int co = (wave * 2 + c) * 16 + 4 * g;
-    float bias[4];
+    for (int c = 0; c < 2; ++c) {
+      const int co = (wave * 2 + c) * 16 + 4 * g;
+      float bias[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) bias[i] = a.bias[l * 128 + co + i];
+      for (int i = 0; i < 4; ++i) bias[i] = a.bias[l * 128 + co + i];
 #pragma unroll
-    for (int p = 0; p < 8; ++p) {
-      const int n = n0 + p * 16 + (lane & 15);
-      if (n >= a.N) continue;
-      store4<T>(out + (((size_t)l * a.B + b) * a.N + n) * 128 + co, acc[c][p][0] + bias[0], acc[c][p][1] + bias[1],
-                acc[c][p][2] + bias[2], acc[c][p][3] + bias[3]);
+      for (int p = 0; p < 8; ++p)
+        store4<T>((T*)(tl + (p * 16 + (lane & 15)) * RS) + co, acc[c][p][0] + bias[0], acc[c][p][1] + bias[1],
+                  acc[c][p][2] + bias[2], acc[c][p][3] + bias[3]);
+    }
+    __syncthreads();
+    const int rows = min(DW_MS, a.N - n0);
+    char* dst = (char*)(out + (((size_t)l * a.B + b) * a.N + n0) * 128);
+#pragma unroll
+    for (int k = 0; k < DW_MS * 16 / 256; ++k) {    // 16 x 16 B per row
+      const int u = tid + k * 256, r = u >> 4, q = u & 15;
+      if (r < rows) *(f32x4*)(dst + r * 256 + q * 16) = *(const f32x4*)(tl + r * RS + q * 16);
+    }
+  } else {
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      const int co = (wave * 2 + c) * 16 + 4 * g;
+      float bias[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bias[i] = a.bias[l * 128 + co + i];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) {
+        const int n = n0 + p * 16 + (lane & 15);
+        if (n >= a.N) continue;
+        store4<T>(out + (((size_t)l * a.B + b) * a.N + n) * 128 + co, acc[c][p][0] + bias[0], acc[c][p][1] + bias[1],
+                  acc[c][p][2] + bias[2], acc[c][p][3] + bias[3]);
+      }
     }
   }
 }
 
 hipError_t launch_dw_cond(int dtype, const DWCondArgs& a, hipStream_t s) {
   if (a.Kp % 32) return hipErrorInvalidValue;
-  const dim3 grid((a.N + DW_MS - 1) / DW_MS, a.B, a.L);
+  const int ntl = (a.N + DW_MS - 1) / DW_MS * a.B;
+  const dim3 grid((unsigned)((ntl + 7) / 8 * 8 * a.L));
   if (dtype == DT_F32) hipLaunchKernelGGL(dw_cond_kernel<float>, grid, dim3(256), 0, s, a);
   else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_cond_kernel<bf16_t>, grid, dim3(256), 0, s, a);
   else hipLaunchKernelGGL(dw_cond_kernel<f16_t>, grid, dim3(256), 0, s, a);
