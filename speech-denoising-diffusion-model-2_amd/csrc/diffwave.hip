@@ -439,6 +439,112 @@ __global__ __launch_bounds__(256, (PREW || sizeof(T) == 4) ? 2 : 3) void dw_laye
   }
 }
 
+// ---------------- GEMM-group tile body shared by the ping-pong and dilation-chain layers ----------------
+template <typename T> using dw_v4 = T __attribute__((ext_vector_type(4)));
+
+// conditioner rows (gate cg.., filter cg+64..) of FPW 16-sample fragments from p0 of tile (b, n0)
+template <typename T, int FPW>
+__device__ __forceinline__ void dw_cond_rows(const DWLayerArgs& a, int b, int n0, int p0, int cg, int lane,
+                                             dw_v4<T> (&cnd)[2][FPW]) {
+  const int N = a.N;
+  const T* cb = (const T*)a.cond + (size_t)a.layer * a.B * N * 128;   // layer-major: one stream per layer
+#pragma unroll
+  for (int p = 0; p < FPW; ++p) {
+    const int n = min(n0 + (p0 + p) * 16 + (lane & 15), N - 1);
+    const T* cp = cb + ((size_t)b * N + n) * 128;
+    cnd[0][p] = *(const dw_v4<T>*)(cp + cg);
+    cnd[1][p] = *(const dw_v4<T>*)(cp + cg + 64);
+  }
+}
+
+// part 1: dilated-conv GEMM over the three tap images tb[t] (plane stride PL), gate, z -> LDS zl and
+// to the layer's z rows (deferred skip GEMM)
+template <typename T, int FPW>
+__device__ __forceinline__ void dw_tile_gate(const DWLayerArgs& a, const char* const (&tb)[3], int PL, char* zl, int b,
+                                             int n0, int p0, int cg, int lane, const Frag<T> (&aw1)[6][2],
+                                             const float (&bg)[4], const float (&bfl)[4],
+                                             const dw_v4<T> (&cnd)[2][FPW]) {
+  constexpr int VE = 8, ES = 2, PLANE = DW_MS * 16;
+  const int N = a.N, g = lane >> 4;
+  f32x4 acc[2][FPW];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 6; ++s) {
+    const int tap = s >> 1, half = s & 1;
+    const char* pb = tb[tap] + ((half * 32 + g * 8) / VE) * PL + (lane & 15) * 16;
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) {
+      const Frag<T> bf = load_planes<T>(pb + (p0 + p) * 256, PL);
+#pragma unroll
+      for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], aw1[s][c], bf);
+    }
+  }
+  const bool full = n0 + DW_MS <= N;
+#pragma unroll
+  for (int p = 0; p < FPW; ++p) {
+    float z[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float gate = acc[0][p][i] + bg[i] + to_f32<T>(cnd[0][p][i]);
+      const float filt = acc[1][p][i] + bfl[i] + to_f32<T>(cnd[1][p][i]);
+      z[i] = dw_sigmoid_fast(gate) * dw_tanh_fast(filt);
+    }
+    store4<T>((T*)(zl + (cg / VE) * PLANE + ((p0 + p) * 16 + (lane & 15)) * 16 + (cg % VE) * ES), z[0], z[1], z[2], z[3]);
+    const int n = n0 + (p0 + p) * 16 + (lane & 15);
+    if (full || n < N) store4<T>((T*)a.z + (((size_t)a.layer * a.B + b) * N + n) * DW_C + cg, z[0], z[1], z[2], z[3]);
+  }
+}
+
+// part 2: output_residual GEMM from zl, epilogue (x + residual) / sqrt(2) with the raw rows xl
+template <typename T, int FPW>
+__device__ __forceinline__ void dw_tile_out(const DWLayerArgs& a, const char* zl, const char* xl, int b, int n0, int p0,
+                                            int cg, int lane, const Frag<T> (&aw2)[2], const float (&br)[4]) {
+  constexpr int VE = 8, ES = 2, PLANE = DW_MS * 16, XS = DW_C * ES + 16;
+  const int N = a.N, g = lane >> 4;
+  const float ir2 = 0.707106769084930419921875f;   // (float)(1 / sqrt(2.0)), as dw_layer_kernel's 16-bit path
+  f32x4 acc[FPW];
+#pragma unroll
+  for (int p = 0; p < FPW; ++p) acc[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const char* pb = zl + ((s * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
+#pragma unroll
+    for (int p = 0; p < FPW; ++p) mfma_frag(acc[p], aw2[s], load_planes<T>(pb + (p0 + p) * 256, PLANE));
+  }
+  const bool full = n0 + DW_MS <= N;
+  T* xo = (T*)a.x_out + (size_t)b * N * DW_C;
+#pragma unroll
+  for (int p = 0; p < FPW; ++p) {
+    const int n = n0 + (p0 + p) * 16 + (lane & 15);
+    if (!full && n >= N) continue;
+    const dw_v4<T> xv = *(const dw_v4<T>*)(xl + ((p0 + p) * 16 + (lane & 15)) * XS + cg * ES);
+    store4<T>(xo + (size_t)n * DW_C + cg, (to_f32<T>(xv[0]) + (acc[p][0] + br[0])) * ir2,
+              (to_f32<T>(xv[1]) + (acc[p][1] + br[1])) * ir2, (to_f32<T>(xv[2]) + (acc[p][2] + br[2])) * ir2,
+              (to_f32<T>(xv[3]) + (acc[p][3] + br[3])) * ir2);
+  }
+}
+
+// the GEMM group's registers: both GEMMs' weight fragments and biases of channel quarter wq
+template <typename T>
+__device__ __forceinline__ void dw_gemm_regs(const DWLayerArgs& a, int wq, int lane, Frag<T> (&aw1)[6][2],
+                                             Frag<T> (&aw2)[2], float (&bg)[4], float (&bfl)[4], float (&br)[4]) {
+  const int g = lane >> 4, cg = wq * 16 + 4 * g;
+  const T* w1 = (const T*)a.w1;
+  const T* w2 = (const T*)a.w2;
+#pragma unroll
+  for (int s = 0; s < 6; ++s)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+      aw1[s][c] = load_frag<T>((const char*)(w1 + (size_t)(c * 64 + wq * 16 + (lane & 15)) * 192 + s * 32 + g * 8));
+#pragma unroll
+  for (int s = 0; s < 2; ++s) aw2[s] = load_frag<T>((const char*)(w2 + (size_t)(wq * 16 + (lane & 15)) * DW_C + s * 32 + g * 8));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) { bg[i] = a.b1[cg + i]; bfl[i] = a.b1[cg + 64 + i]; br[i] = a.b2[cg + i]; }
+}
+
 // ---------------- ping-pong residual layer (16-bit) ----------------
 // The same layer as dw_layer_kernel, with the staging and the GEMMs of a CU split between two wave
 // groups that work on different tiles: a persistent block of 8 waves walks a strided list of
@@ -533,91 +639,148 @@ __global__ __launch_bounds__(64 * (GW + 4), 1) void dw_layer_pp_kernel(DWLayerAr
   // ---------------- GEMM group: wave = channel quarter wq x sample part (FPW fragments from p0) ----------------
   const int wq = wave & 3, p0 = (wave >> 2) * FPW;
   const int cg = wq * 16 + 4 * g;                // gate rows cg..cg+3; filter rows cg + 64
-  const T* w1 = (const T*)a.w1;
-  const T* w2 = (const T*)a.w2;
   Frag<T> aw1[6][2], aw2[2];
-#pragma unroll
-  for (int s = 0; s < 6; ++s)
-#pragma unroll
-    for (int c = 0; c < 2; ++c)
-      aw1[s][c] = load_frag<T>((const char*)(w1 + (size_t)(c * 64 + wq * 16 + (lane & 15)) * 192 + s * 32 + g * 8));
-#pragma unroll
-  for (int s = 0; s < 2; ++s) aw2[s] = load_frag<T>((const char*)(w2 + (size_t)(wq * 16 + (lane & 15)) * DW_C + s * 32 + g * 8));
   float bg[4], bfl[4], br[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) { bg[i] = a.b1[cg + i]; bfl[i] = a.b1[cg + 64 + i]; br[i] = a.b2[cg + i]; }
-  const float ir2 = 0.707106769084930419921875f;   // (float)(1 / sqrt(2.0)), as dw_layer_kernel's 16-bit path
+  dw_gemm_regs<T>(a, wq, lane, aw1, aw2, bg, bfl, br);
   // conditioner rows of this wave's channels: loaded one tile ahead (issued after the gate of the
   // previous tile, so they are in flight during its output_residual GEMM, epilogue and barriers)
-  vec4 cnd[2][FPW];
-  const T* cb = (const T*)a.cond + (size_t)a.layer * a.B * N * 128;   // layer-major: one stream per layer
-  auto load_cond = [&](int tl) {
-    const int b = tl / tpc, n0 = (tl - b * tpc) * DW_MS;
-#pragma unroll
-    for (int p = 0; p < FPW; ++p) {
-      const int n = min(n0 + (p0 + p) * 16 + (lane & 15), N - 1);
-      const T* cp = cb + ((size_t)b * N + n) * 128;
-      cnd[0][p] = *(const vec4*)(cp + cg);
-      cnd[1][p] = *(const vec4*)(cp + cg + 64);
-    }
-  };
-  if (tile < ntiles) load_cond(tile);
+  dw_v4<T> cnd[2][FPW];
+  if (tile < ntiles) dw_cond_rows<T, FPW>(a, tile / tpc, (tile % tpc) * DW_MS, p0, cg, lane, cnd);
   lds_sync();                                      // tile 0 staged
   for (int k = 0; tile < ntiles; ++k, tile += G) {
     const int b = tile / tpc, n0 = (tile - b * tpc) * DW_MS;
     const char* yin = smem + (k & 1) * DW_PP_SLOT;
-    const char* xl = yin + DW_PP_Y;
-    f32x4 acc[2][FPW];
+    const char* tb[3];
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
-#pragma unroll
-      for (int p = 0; p < FPW; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 6; ++s) {
-      const int tap = s >> 1, half = s & 1;
-      const char* pb = yin + ((win ? 0 : tap * UPS) + (half * 32 + g * 8) / VE) * PL + ((win ? tap * d : 0) + (lane & 15)) * 16;
-#pragma unroll
-      for (int p = 0; p < FPW; ++p) {
-        const Frag<T> bf = load_planes<T>(pb + (p0 + p) * 256, PL);
-#pragma unroll
-        for (int c = 0; c < 2; ++c) mfma_frag(acc[c][p], aw1[s][c], bf);
-      }
-    }
-    const bool full = n0 + DW_MS <= N;
-#pragma unroll
-    for (int p = 0; p < FPW; ++p) {
-      float z[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const float gate = acc[0][p][i] + bg[i] + to_f32<T>(cnd[0][p][i]);
-        const float filt = acc[1][p][i] + bfl[i] + to_f32<T>(cnd[1][p][i]);
-        z[i] = dw_sigmoid_fast(gate) * dw_tanh_fast(filt);
-      }
-      store4<T>((T*)(zl + (cg / VE) * PLANE + ((p0 + p) * 16 + (lane & 15)) * 16 + (cg % VE) * ES), z[0], z[1], z[2], z[3]);
-      const int n = n0 + (p0 + p) * 16 + (lane & 15);
-      if (full || n < N) store4<T>((T*)a.z + (((size_t)a.layer * a.B + b) * N + n) * DW_C + cg, z[0], z[1], z[2], z[3]);
-    }
-    if (tile + G < ntiles) load_cond(tile + G);
+    for (int t = 0; t < 3; ++t) tb[t] = yin + (win ? t * d * 16 : t * UPS * PL);
+    dw_tile_gate<T, FPW>(a, tb, PL, zl, b, n0, p0, cg, lane, aw1, bg, bfl, cnd);
+    if (tile + G < ntiles) dw_cond_rows<T, FPW>(a, (tile + G) / tpc, ((tile + G) % tpc) * DW_MS, p0, cg, lane, cnd);
     lds_sync();                                    // z hand-off (the z stores and next conditioner loads stay in flight)
-#pragma unroll
-    for (int p = 0; p < FPW; ++p) acc[0][p] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const char* pb = zl + ((s * 32 + g * 8) / VE) * PLANE + (lane & 15) * 16;
-#pragma unroll
-      for (int p = 0; p < FPW; ++p) mfma_frag(acc[0][p], aw2[s], load_planes<T>(pb + (p0 + p) * 256, PLANE));
-    }
-    T* xo = (T*)a.x_out + (size_t)b * N * DW_C;
-#pragma unroll
-    for (int p = 0; p < FPW; ++p) {
-      const int n = n0 + (p0 + p) * 16 + (lane & 15);
-      if (!full && n >= N) continue;
-      const vec4 xv = *(const vec4*)(xl + ((p0 + p) * 16 + (lane & 15)) * XS + cg * ES);
-      store4<T>(xo + (size_t)n * DW_C + cg, (to_f32<T>(xv[0]) + (acc[0][p][0] + br[0])) * ir2,
-                (to_f32<T>(xv[1]) + (acc[0][p][1] + br[1])) * ir2, (to_f32<T>(xv[2]) + (acc[0][p][2] + br[2])) * ir2,
-                (to_f32<T>(xv[3]) + (acc[0][p][3] + br[3])) * ir2);
-    }
+    dw_tile_out<T, FPW>(a, zl, yin + DW_PP_Y, b, n0, p0, cg, lane, aw2, br);
     lds_sync();                                    // slot swap
+  }
+}
+
+// ---------------- dilation-chain residual layer (16-bit, dilation a multiple of 128) ----------------
+// For d >= 128 the three taps of a 128-sample tile are three disjoint 128-row images, so a tile of
+// the ping-pong kernel stages three images.  Here a block walks a dilation chain -- tiles n0, n0 + d,
+// n0 + 2d, ... of one clip, whose taps are images n0 - d, n0, n0 + d -- in segments of DW_CH_SEG
+// tiles and keeps the images in a ring of four LDS slots: after a segment's first tile every tile
+// stages ONE new image (its successor's +d tap), the GEMM group reads the other three.  An image
+// slot also holds the raw rows (the residual, when the image is a tile's centre).  Same wave groups,
+// barriers and GEMM-group body as the ping-pong kernel.  A segment's first tile waits for its three
+// images (no overlap), so segments are long: d >= 128 layers 213 -> 199 / 190 / 185 us at 8 / 16 /
+// 32 tiles per segment (config #3; the d <= 64 ping-pong layers: 182-189 us).
+constexpr int DW_CH_IMG = 8 * DW_MS * 16;                      // y image: 8 planes x 128 rows x 16 B
+constexpr int DW_CH_SLOT = DW_CH_IMG + DW_MS * (DW_C * 2 + 16);  // + raw rows
+constexpr int DW_CH_LDS = 4 * DW_CH_SLOT + 8 * DW_MS * 16;      // ring of four + z
+
+template <typename T, int DW_CH_SEG>                           // tiles per chain segment
+__global__ __launch_bounds__(512, 1) void dw_layer_chain_kernel(DWLayerArgs a) {
+  static_assert(sizeof(T) == 2, "16-bit only");
+  constexpr int VE = 8, PB = 8, PLANE = DW_MS * 16, XS = DW_C * 2 + 16, FPW = 8;
+  typedef T vec __attribute__((ext_vector_type(VE)));
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* zl = smem + 4 * DW_CH_SLOT;
+  const int tid = threadIdx.x, lane = tid & 63, g = lane >> 4;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int N = a.N, d = a.dil, G = gridDim.x;
+  const int tpc = (N + DW_MS - 1) / DW_MS, R = d / DW_MS;          // chains per clip
+  const int t_now = a.t_dev ? *a.t_dev : 0;
+  // segments per clip: chain rho has ceil((tpc - rho) / R) tiles
+  int spc = 0;
+  for (int rho = 0; rho < R && rho < tpc; ++rho) spc += ((tpc - rho + R - 1) / R + DW_CH_SEG - 1) / DW_CH_SEG;
+  const int nseg = spc * a.B;
+  // segment id -> clip b, chain rho, first chain index j0, tile count len
+  auto segment = [&](int sid, int& b, int& rho, int& j0, int& len) {
+    b = sid / spc;
+    int r = sid - b * spc;
+    rho = 0;
+    for (;; ++rho) {
+      const int nj = (tpc - rho + R - 1) / R, ns = (nj + DW_CH_SEG - 1) / DW_CH_SEG;
+      if (r < ns) { j0 = r * DW_CH_SEG; len = min(DW_CH_SEG, nj - j0); return; }
+      r -= ns;
+    }
+  };
+  // image m of a segment (m = -1 .. len): rows nb + m d with nb = the first tile's n0; ring slot (m + 1) & 3
+  auto slot = [&](int m) { return smem + ((m + 1) & 3) * DW_CH_SLOT; };
+
+  if (wave >= 4) {
+    // ---------------- staging group: one 1024-unit image = 4 units per thread ----------------
+    const int st = tid - 256;
+    const int qs = (st & 63) / PB;
+    f32x4 reg[12];
+    float dsv[VE];
+    // loads of images m0 .. m0 + cnt - 1 (cnt <= 3) into reg[4 i ..]
+    auto issue = [&](const T* xin, int nb, int m0, int cnt) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        if (k / 4 < cnt) {
+          const int u = st + (k & 3) * 256, grp = u >> 6, j = u & 63, q = j / PB, s = grp * PB + (j % PB);
+          const int n = nb + (m0 + k / 4) * d + s;
+          reg[k] = *(const f32x4*)(xin + (size_t)min(max(n, 0), N - 1) * DW_C + q * VE);
+        }
+      }
+    };
+    auto land = [&](int nb, int m0, int cnt) {
+#pragma unroll
+      for (int k = 0; k < 12; ++k) {
+        if (k / 4 < cnt) {
+          const int u = st + (k & 3) * 256, grp = u >> 6, j = u & 63, q = j / PB, s = grp * PB + (j % PB);
+          const int m = m0 + k / 4, n = nb + m * d + s;
+          const bool ok = n >= 0 && n < N;
+          char* sl = slot(m);
+          *(f32x4*)(sl + DW_CH_IMG + s * XS + q * 16) = reg[k];
+          vec v = __builtin_bit_cast(vec, reg[k]);
+#pragma unroll
+          for (int e = 0; e < VE; ++e) v[e] = from_f32<T>(ok ? to_f32<T>(v[e]) + dsv[e] : 0.f);
+          *(f32x4*)(sl + q * PLANE + s * 16) = __builtin_bit_cast(f32x4, v);
+        }
+      }
+    };
+    for (int sid = blockIdx.x; sid < nseg; sid += G) {
+      int b, rho, j0, len;
+      segment(sid, b, rho, j0, len);
+      const int nb = (rho + j0 * R) * DW_MS;
+      const T* xin = (const T*)a.x_in + (size_t)b * N * DW_C;
+      const float* ds = a.ds + ((size_t)(a.ds_per_b ? b : t_now) * a.L + a.layer) * DW_C;
+#pragma unroll
+      for (int e = 0; e < VE; ++e) dsv[e] = ds[qs * VE + e];
+      issue(xin, nb, -1, 3);                       // images -1, 0, 1: the first tile's taps
+      land(nb, -1, 3);
+      lds_sync();                                  // segment start
+      for (int i = 0; i < len; ++i) {
+        if (i + 1 < len) issue(xin, nb, i + 2, 1);
+        lds_sync();                                // (the GEMM group's z hand-off; the loads stay in flight)
+        if (i + 1 < len) land(nb, i + 2, 1);
+        lds_sync();                                // tile done
+      }
+    }
+    return;
+  }
+
+  // ---------------- GEMM group ----------------
+  const int wq = wave & 3, p0 = 0;
+  const int cg = wq * 16 + 4 * g;
+  Frag<T> aw1[6][2], aw2[2];
+  float bg[4], bfl[4], br[4];
+  dw_gemm_regs<T>(a, wq, lane, aw1, aw2, bg, bfl, br);
+  dw_v4<T> cnd[2][FPW];
+  for (int sid = blockIdx.x; sid < nseg; sid += G) {
+    int b, rho, j0, len;
+    segment(sid, b, rho, j0, len);
+    const int nb = (rho + j0 * R) * DW_MS;
+    dw_cond_rows<T, FPW>(a, b, nb, p0, cg, lane, cnd);
+    lds_sync();                                    // segment start: the first tile's images staged
+    for (int i = 0; i < len; ++i) {
+      const int n0 = nb + i * d;
+      const char* tb[3] = {slot(i - 1), slot(i), slot(i + 1)};
+      dw_tile_gate<T, FPW>(a, tb, PLANE, zl, b, n0, p0, cg, lane, aw1, bg, bfl, cnd);
+      if (i + 1 < len) dw_cond_rows<T, FPW>(a, b, n0 + d, p0, cg, lane, cnd);
+      lds_sync();                                  // z hand-off
+      dw_tile_out<T, FPW>(a, zl, slot(i) + DW_CH_IMG, b, n0, p0, cg, lane, aw2, br);
+      lds_sync();                                  // tile done
+    }
   }
 }
 
@@ -646,6 +809,23 @@ hipError_t launch_dw_layer(int dtype, const DWLayerArgs& a, hipStream_t s) {
     }
     const int ntiles = (int)grid.x * (int)grid.y;
     const dim3 pgrid(ntiles < ncu ? ntiles : ncu);
+    static const bool nochain = std::getenv("SDDM_DW_NOCHAIN") != nullptr;   // A/B knob
+    if (!nochain && a.dil % DW_MS == 0) {          // dilation chains (d >= 128)
+      static const int seg = std::getenv("SDDM_DW_CHSEG") ? std::atoi(std::getenv("SDDM_DW_CHSEG")) : 32;   // A/B knob (8 / 16 / 32)
+      const int tpc = (a.N + DW_MS - 1) / DW_MS, R = a.dil / DW_MS;
+      int spc = 0;
+      for (int rho = 0; rho < R && rho < tpc; ++rho) spc += ((tpc - rho + R - 1) / R + seg - 1) / seg;
+      const int nseg = spc * a.B;
+      const dim3 cgrid(nseg < ncu ? nseg : ncu);
+#define SDDM_DW_CHAIN(S)                                                                                          \
+  if (dtype == DT_BF16) hipLaunchKernelGGL((dw_layer_chain_kernel<bf16_t, S>), cgrid, dim3(512), DW_CH_LDS, s, a); \
+  else hipLaunchKernelGGL((dw_layer_chain_kernel<f16_t, S>), cgrid, dim3(512), DW_CH_LDS, s, a);
+      if (seg == 32) { SDDM_DW_CHAIN(32) }
+      else if (seg == 16) { SDDM_DW_CHAIN(16) }
+      else { SDDM_DW_CHAIN(8) }
+#undef SDDM_DW_CHAIN
+      return hipGetLastError();
+    }
     if (dtype == DT_BF16) hipLaunchKernelGGL((dw_layer_pp_kernel<bf16_t, 4>), pgrid, dim3(512), DW_PP_LDS, s, a);
     else hipLaunchKernelGGL((dw_layer_pp_kernel<f16_t, 4>), pgrid, dim3(512), DW_PP_LDS, s, a);
     return hipGetLastError();
