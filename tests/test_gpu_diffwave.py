@@ -113,6 +113,25 @@ def test_diffwave_config3_bench_batch(torch_cuda):
         assert err <= 3e-2 * max(1.0, rms(ref[i], 0))
 
 
+@pytest.mark.parametrize("dtype,tol", [("bfloat16", 3e-2), ("float16", 5e-3)])
+@pytest.mark.parametrize("F", [1, 2, 5])
+def test_diffwave_short_clips_dilation_chains(torch_cuda, dtype, tol, F):
+    """Clips of 1 / 2 / 5 frames (256 / 512 / 1280 samples = 2 / 4 / 10 tiles of 128): the
+    dilation-chain layers (d = 128 .. 512, dw_layer_chain_kernel) then have fewer tiles per clip
+    than chains (d / 128), one-tile chains whose -d / +d tap images lie wholly outside the clip,
+    and chains of uneven length; every row against the numpy oracle."""
+    from oracle import diffwave as odw
+    B = 3
+    spec, audio, steps = _dw_rows(B, F, 40 + F)
+    ref = odw.forward(diffwave_params(), spec, audio, steps)
+    eps = _net(dtype)(torch.from_numpy(spec).cuda(), torch.from_numpy(audio).cuda(),
+                      torch.from_numpy(steps).reshape(-1, 1, 1).cuda()).cpu().numpy()
+    for b in range(B):
+        err = rms(eps[b], ref[b])
+        print(f"{dtype} F={F} row {b}: rms {err:.3e} (ref rms {rms(ref[b], 0):.3f})")
+        assert np.isfinite(eps[b]).all() and err <= tol * max(1.0, rms(ref[b], 0))
+
+
 def test_spectrogram_bin_count_is_checked(torch_cuda):
     """An 80-bin mel condition for a 513-bin DiffWave raises (the reference's Conv1d(freq_bins, ...)
     rejects it) instead of being read out of bounds by the library."""
