@@ -911,31 +911,54 @@ hipError_t launch_dw_skip(int dtype, const DWSkipArgs& a, hipStream_t s) {
 }
 
 // ---------------- output: skip sum / sqrt(L) -> skip_projection -> relu -> output_projection ----------------
+// diffwave.py:150-155 per sample: h = Wsp (skip / sqrt(L)) + bsp, eps = wop . relu(h) + bop.  The
+// 64 x 64 skip_projection runs as fp32 MFMA (16x16x4 f32): a wave = 64 samples x all 64 outputs
+// (4 x 4 tiles, K = 64 in two 32-deep fragments), B fragments = 32-byte pieces of the samples' skip
+// rows scaled by 1 / sqrt(L) (as the reference divides before the projection); relu and
+// output_projection from the accumulators, the 64-output sum reduced over the 4 lane groups.
 __global__ __launch_bounds__(256) void dw_output_kernel(DWOutArgs a) {
-  __shared__ float wsp[DW_C * DW_C], bsp[DW_C], wop[DW_C];
-  const int tid = threadIdx.x;
-  for (int i = tid; i < DW_C * DW_C; i += 256) wsp[i] = a.wsp[i];
-  if (tid < DW_C) { bsp[tid] = a.bsp[tid]; wop[tid] = a.wop[tid]; }
-  __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * 256 + tid;
-  if (i >= a.total) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int64_t n0 = (int64_t)blockIdx.x * 256 + wave * 64;
   const float rl = a.sqrt_layers;
-  float s[DW_C];
-  const f32x4* sp = (const f32x4*)(a.skip + i * DW_C);
+  f32x4 acc[4][4];
 #pragma unroll
-  for (int q = 0; q < DW_C / 4; ++q) {
-    const f32x4 v = sp[q];
+  for (int c = 0; c < 4; ++c)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s[q * 4 + e] = v[e] / rl;
+    for (int p = 0; p < 4; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {                    // K = 64 in two 32-deep fragments
+    Frag<float> af[4], bf[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) af[c] = load_frag<float>((const char*)(a.wsp + (c * 16 + l16) * DW_C + h * 32 + g * 8));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      const int64_t n = min(n0 + p * 16 + l16, a.total - 1);
+      bf[p] = load_frag<float>((const char*)(a.skip + n * DW_C + h * 32 + g * 8));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { bf[p].lo[e] = bf[p].lo[e] / rl; bf[p].hi[e] = bf[p].hi[e] / rl; }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) mfma_frag(acc[c][p], af[c], bf[p]);
   }
-  float out = a.bop[0];
-  for (int o = 0; o < DW_C; ++o) {
-    float h = bsp[o];
+  float bs[4][4], wo[4][4];                        // this lane's 16 outputs o = 16 c + 4 g + i
 #pragma unroll
-    for (int c = 0; c < DW_C; ++c) h += wsp[o * DW_C + c] * s[c];
-    out += wop[o] * fmaxf(h, 0.f);
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { bs[c][i] = a.bsp[c * 16 + 4 * g + i]; wo[c][i] = a.wop[c * 16 + 4 * g + i]; }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    float part = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) part += wo[c][i] * fmaxf(acc[c][p][i] + bs[c][i], 0.f);
+    part += __shfl_xor(part, 16);
+    part += __shfl_xor(part, 32);
+    const int64_t n = n0 + p * 16 + l16;
+    if (g == 0 && n < a.total) a.eps[n] = a.bop[0] + part;
   }
-  a.eps[i] = out;
 }
 
 hipError_t launch_dw_output(const DWOutArgs& a, hipStream_t s) {
