@@ -910,6 +910,102 @@ hipError_t launch_dw_skip(int dtype, const DWSkipArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------- deferred skip sum fused with the output head ----------------
+// dw_skip_kernel's GEMM, then the head of dw_output_kernel straight from the accumulators: lane
+// (g, l16) holds s[co = 16 c + 4 g + i][n = l16] of each tile, which is exactly the B operand of a
+// 16x16x4 f32 MFMA step whose four k values are {16 c + 4 g' + i : g' = 0..3} -- so skip_projection
+// consumes the skip sum from registers (16 steps per 16 outputs), and the fp32 skip rows never go
+// to HBM (264 MB written and read again per step at config #3).
+template <typename T>
+__global__ __launch_bounds__(256) void dw_skip_head_kernel(DWSkipArgs a, DWOutArgs o) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int n0 = blockIdx.x * 256 + wave * 64, b = blockIdx.y, K = a.L * DW_C;
+  const size_t LS = (size_t)a.B * a.N * DW_C;        // z is layer-major: [L][B][N][64]
+  const T* Z = (const T*)a.z + (size_t)b * a.N * DW_C;
+  const T* arow[4];
+  const T* brow[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) arow[c] = (const T*)a.w + (size_t)(c * 16 + l16) * K + g * 8;
+#pragma unroll
+  for (int p = 0; p < 4; ++p) brow[p] = Z + (size_t)min(n0 + p * 16 + l16, a.N - 1) * DW_C + g * 8;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int p = 0; p < 4; ++p) acc[c][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frag<T> af[4], bf[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) af[c] = load_frag<T>((const char*)arow[c]);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) bf[p] = load_frag<T>((const char*)brow[p]);
+  for (int k = 0; k < K; k += 32) {
+    const int kn = k + 32 < K ? k + 32 : k;
+    Frag<T> an[4], bn[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) an[c] = load_frag<T>((const char*)(arow[c] + kn));
+#pragma unroll
+    for (int p = 0; p < 4; ++p) bn[p] = load_frag<T>((const char*)(brow[p] + (size_t)(kn >> 6) * LS + (kn & 63)));
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int p = 0; p < 4; ++p) mfma_frag(acc[c][p], af[c], bf[p]);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) af[c] = an[c];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) bf[p] = bn[p];
+  }
+  // skip sum / sqrt(L), as the reference divides before skip_projection
+  const float rl = o.sqrt_layers;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float bias[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bias[i] = a.bias[c * 16 + 4 * g + i];
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[c][p][i] = (acc[c][p][i] + bias[i]) / rl;
+  }
+  float part[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int oc = 0; oc < 4; ++oc) {                 // outputs 16 oc .. 16 oc + 15
+    f32x4 h[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) h[p] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float w = o.wsp[(oc * 16 + l16) * DW_C + c * 16 + 4 * g + i];
+#pragma unroll
+        for (int p = 0; p < 4; ++p) h[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(w, acc[c][p][i], h[p], 0, 0, 0);
+      }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int oo = oc * 16 + 4 * g + i;
+      const float bs = o.bsp[oo], wo = o.wop[oo];
+#pragma unroll
+      for (int p = 0; p < 4; ++p) part[p] += wo * fmaxf(h[p][i] + bs, 0.f);
+    }
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    float v = part[p];
+    v += __shfl_xor(v, 16);
+    v += __shfl_xor(v, 32);
+    const int n = n0 + p * 16 + l16;
+    if (g == 0 && n < a.N) o.eps[(size_t)b * a.N + n] = o.bop[0] + v;
+  }
+}
+
+hipError_t launch_dw_skip_head(int dtype, const DWSkipArgs& a, const DWOutArgs& o, hipStream_t s) {
+  const dim3 grid((a.N + 255) / 256, a.B);
+  if (dtype == DT_F32) hipLaunchKernelGGL(dw_skip_head_kernel<float>, grid, dim3(256), 0, s, a, o);
+  else if (dtype == DT_BF16) hipLaunchKernelGGL(dw_skip_head_kernel<bf16_t>, grid, dim3(256), 0, s, a, o);
+  else hipLaunchKernelGGL(dw_skip_head_kernel<f16_t>, grid, dim3(256), 0, s, a, o);
+  return hipGetLastError();
+}
+
 // ---------------- output: skip sum / sqrt(L) -> skip_projection -> relu -> output_projection ----------------
 // diffwave.py:150-155 per sample: h = Wsp (skip / sqrt(L)) + bsp, eps = wop . relu(h) + bop.  The
 // 64 x 64 skip_projection runs as fp32 MFMA (16x16x4 f32): a wave = 64 samples x all 64 outputs

@@ -3,6 +3,11 @@
 // model/diffwave.py).  Kernels: diffwave.hip.
 #pragma once
 
+namespace sddm {
+// deferred skip GEMM + output head in one launch (diffwave.hip)
+hipError_t launch_dw_skip_head(int dtype, const DWSkipArgs& a, const DWOutArgs& o, hipStream_t s);
+}  // namespace sddm
+
 struct DWState {
   int C = 64, L = 30, cycle = 10, bins = 513, hop = 256, Kp = 544;
   std::map<std::string, size_t> woff;   // packed weights in ctx->warena
@@ -248,14 +253,19 @@ static int dw_network(sddm_ctx* c, const float* audio, int B, int F, const float
   DWSkipArgs sk{};
   sk.z = d.act.base + d.off_z; sk.w = W.base + d.woff.at("skip.w"); sk.bias = W.at<float>(d.woff.at("skip.b"));
   sk.skip = d.act.at<float>(d.off_skip); sk.B = B; sk.N = N; sk.L = d.L;
-  SDDM_HIP_CHECK(launch_dw_skip(c->dtype, sk, s));
   DWOutArgs o{};
   o.skip = d.act.at<float>(d.off_skip);
   o.wsp = W.at<float>(d.woff.at("sp.w")); o.bsp = W.at<float>(d.woff.at("sp.b"));
   o.wop = W.at<float>(d.woff.at("op.w")); o.bop = W.at<float>(d.woff.at("op.b"));
   o.sqrt_layers = (float)std::sqrt((double)d.L);
   o.eps = d.act.at<float>(d.off_eps); o.total = (int64_t)B * N;
-  SDDM_HIP_CHECK(launch_dw_output(o, s));
+  static const bool nofuse = std::getenv("SDDM_DW_NOFUSE") != nullptr;   // A/B knob: skip rows via HBM
+  if (nofuse) {
+    SDDM_HIP_CHECK(launch_dw_skip(c->dtype, sk, s));
+    SDDM_HIP_CHECK(launch_dw_output(o, s));
+  } else {
+    SDDM_HIP_CHECK(launch_dw_skip_head(c->dtype, sk, o, s));
+  }
   return SDDM_OK;
 }
 
